@@ -1,0 +1,267 @@
+"""LEGACY Monte Carlo benchmark (BASELINE.json metric: panels/s at the sf_e_110 shape).
+
+One "step" = one pass of the hot path (analysis.py:162-191) over one batch of
+synthetic-instance panels per GPU, entirely on the device:
+draw (with restarts) -> per-person counts -> pair counts X^T X (int8 MFMA) ->
+distinct-panel count, plus (N > 1) the RCCL exchange (all_reduce of counts and
+pairs, all_gather of panel hashes + device owner dedupe + all_reduce).
+
+    python bench.py [--gpus N --steps K --warmup W] [--config sf_e_110] [--panels P]
+
+Default workload: BASELINE config 2 -- the sf_e_110-shape instance
+(tests/golden/instances/sf_e_110, n=1727 k=110 C=7 F=31; synthetic, the real
+pool is withheld) at 10^6 panels per GPU per step (weak scaling).  Rank 0
+prints ONE JSON line.  The instance and every buffer are resident in HBM
+before the timed region.
+"""
+import argparse
+import ctypes
+import glob
+import importlib
+import json
+import os
+import platform
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+PKG = "citizensassemblies-replication_amd"
+
+HBM_PEAK = 8.0e12          # B/s, MI355X spec (MI355X_MICROARCH.md)
+I8_MFMA_PEAK = 5.03e15     # dense int8 ops/s: 2x the 2.5 PF bf16 dense rate (MI355X_MICROARCH.md)
+
+CONFIGS = {
+    # name: (instance dir, k, default panels per GPU per step)
+    "sf_e_110": ("sf_e_110", 110, 10 ** 6),
+    "example_large_200": ("example_large_200", 200, 10 ** 6),
+    "couples": ("couples_panel_from_twenty_people_no_constraints_2", 2, 10 ** 6),
+    "synthetic8192": ("synthetic8192_200", 200, 10 ** 5),
+    "example_small_20": ("example_small_20", 20, 10 ** 6),
+}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--config", default="sf_e_110", choices=sorted(CONFIGS))
+    ap.add_argument("--panels", type=int, default=0, help="panels per GPU per step (0 = config default)")
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--no-pairs", action="store_true")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample duration")
+    return ap.parse_args()
+
+
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or "unknown"
+
+
+def cpu_baseline(inst_dir, k, seed, target_s, want_pairs):
+    """C oracle (the 'port') on the host cores: draw + counts + pairs + unique on a bounded sample."""
+    from oracle import coracle
+    from oracle.legacy_oracle import read_instance
+    d = os.path.join(REPO, "tests", "golden", "instances", inst_dir)
+    o = read_instance(os.path.join(d, "categories.csv"), os.path.join(d, "respondents.csv"), k)
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
+    threads = max(1, min(threads, 16))
+
+    def run(S):
+        t = time.perf_counter()
+        rc, panels, _, _ = coracle.draw(o, k, seed, 0, S, threads=threads)
+        assert rc == 0
+        coracle.counts(panels, o.n)
+        if want_pairs:
+            coracle.pairs(panels, o.n, threads=threads)
+        coracle.unique(panels, o.n)
+        return time.perf_counter() - t
+
+    probe = 2000
+    dt = run(probe)
+    S = int(min(max(probe, probe * target_s / max(dt, 1e-6)), 5 * 10 ** 6))
+    dt = run(S)
+    return {"value": S / dt, "unit": "panels/s", "cores": threads, "kind": "port",
+            "sample": "%d panels of %s (draw+counts+%sunique), C oracle OpenMP x%d on %s" % (
+                S, inst_dir, "pairs+" if want_pairs else "", threads, cpu_model()),
+            "seconds": round(dt, 3)}
+
+
+def load_pmc_traffic(config):
+    """HBM bytes per draw launch from a committed rocprofv3 --pmc summary (tools/pmc_summary.py)."""
+    path = os.path.join(REPO, "profiles", "pmc_%s.json" % config)
+    if not os.path.exists(path):
+        return None
+    with open(path) as fh:
+        return json.load(fh)
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and rank == 0:
+        print("warning: --gpus %d but WORLD_SIZE %d" % (args.gpus, world), file=sys.stderr)
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=dev)
+
+    P = importlib.import_module(PKG)
+    Dv = importlib.import_module(PKG + ".device")
+    Dd = importlib.import_module(PKG + ".distributed")
+    inst_dir, k, default_panels = CONFIGS[args.config]
+    S = args.panels or default_panels
+    d = os.path.join(REPO, "tests", "golden", "instances", inst_dir)
+    inst = P.read_instance(os.path.join(d, "categories.csv"), os.path.join(d, "respondents.csv"), k)
+    enc = P.encode(inst.categories, inst.agents)
+    enc.check_quotas(k)
+    want_pairs = not args.no_pairs
+    stream = torch.cuda.current_stream(dev)
+    pipe = Dv.DevicePipeline(enc, k, S, want_pairs=want_pairs, want_unique=True, device=dev, stream=stream)
+    table = Dd.HashTable(S * world, dev) if world > 1 else None
+
+    stages = ["draw", "xt_count", "pairs", "unique", "exchange"]
+    ev_log = []
+
+    def step(i, record):
+        begin = (i * world + rank) * S            # global panel indices, distinct per step and rank
+        evs = [torch.cuda.Event(enable_timing=True) for _ in range(len(stages) + 1)] if record else None
+        pipe.reset()
+        if evs:
+            evs[0].record(stream)
+        pipe.draw(args.seed, begin, S)
+        if evs:
+            evs[1].record(stream)
+        pipe.transpose_count(S)
+        if evs:
+            evs[2].record(stream)
+        if want_pairs:
+            pipe.pair_counts(S)
+        if evs:
+            evs[3].record(stream)
+        if world == 1:
+            pipe.unique_count(S)
+        if evs:
+            evs[4].record(stream)
+        if world > 1:
+            Dd.combine(pipe.counts, pipe.pairs, pipe.hashes[: 2 * S], table=table, stream=stream)
+        if evs:
+            evs[5].record(stream)
+            ev_log.append(evs)
+
+    for i in range(args.warmup):
+        step(i, False)
+    torch.cuda.synchronize()
+    pipe.check_status()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(args.warmup + i, True)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    pipe.check_status()
+    elapsed = t1 - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    # per-stage device time (ms) averaged over the timed steps
+    stage_ms = {s: 0.0 for s in stages}
+    for evs in ev_log:
+        for j, s in enumerate(stages):
+            stage_ms[s] += evs[j].elapsed_time(evs[j + 1]) / len(ev_log)
+    n, W = enc.n, enc.W
+    npad = pipe.npad
+    nblk = (S + 63) // 64
+    draw_bytes = S * (8 * W + 16)                         # packed panel + 128-bit hash per panel
+    xt_bytes = S * 8 * W + nblk * npad * 8 + n * 8        # read panels, write transposed bits + counts
+    pair_ops = S * n * (n + 1)                            # triangle form of 2*S*n^2
+    uniq_bytes = S * (16 + 8 * 2)                         # hashes + table slot traffic (approx.)
+
+    def gbs(b, ms):
+        return b / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
+
+    kernels = {
+        "draw": {"ms": stage_ms["draw"], "panels_per_s": S / (stage_ms["draw"] * 1e-3) if stage_ms["draw"] else 0,
+                 "bound": "issue (VALU/LDS latency)", "hbm_GBps": gbs(draw_bytes, stage_ms["draw"])},
+        "xt_count": {"ms": stage_ms["xt_count"], "hbm_GBps": gbs(xt_bytes, stage_ms["xt_count"]),
+                     "frac": gbs(xt_bytes, stage_ms["xt_count"]) * 1e9 / HBM_PEAK},
+        "unique": {"ms": stage_ms["unique"], "hbm_GBps": gbs(uniq_bytes, stage_ms["unique"])},
+    }
+    if want_pairs:
+        tops = pair_ops / (stage_ms["pairs"] * 1e-3) / 1e12 if stage_ms["pairs"] else 0.0
+        kernels["pairs_mfma"] = {"ms": stage_ms["pairs"], "TOPs": tops, "mfma_util": tops * 1e12 / I8_MFMA_PEAK}
+    if world > 1:
+        kernels["exchange"] = {"ms": stage_ms["exchange"]}
+    dominant = max(("draw", "xt_count", "pairs", "unique"), key=lambda s: stage_ms[s])
+    pmc = load_pmc_traffic(args.config)
+    if dominant == "pairs":
+        ach = pair_ops / (stage_ms["pairs"] * 1e-3) / 1e12
+        roof = {"kernel": "pair_mfma_kernel", "bound": "mfma", "achieved": ach, "peak": I8_MFMA_PEAK / 1e12,
+                "unit": "TFLOP/s", "frac": ach * 1e12 / I8_MFMA_PEAK, "traffic": None}
+    else:
+        name = {"draw": "draw_kernel", "xt_count": "xt_count_kernel", "unique": "unique_kernel"}[dominant]
+        b = {"draw": draw_bytes, "xt_count": xt_bytes, "unique": uniq_bytes}[dominant]
+        ach = gbs(b, stage_ms[dominant])
+        traffic = None
+        if pmc and pmc.get("kernel") == name and pmc.get("panels") == S:
+            traffic = pmc.get("hbm_bytes_per_launch")
+        roof = {"kernel": name, "bound": "hbm", "achieved": ach, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
+                "frac": ach * 1e9 / HBM_PEAK, "traffic": traffic,
+                "note": "draw_kernel is VALU/LDS issue-bound; its HBM bytes are the panel+hash writes"}
+
+    total = S * world * args.steps
+    result = {
+        "metric": "LEGACY panels/sec (node) at sf_e_110 shape; XtX MFMA util; speedup vs CPU",
+        "value": total / elapsed,
+        "unit": "panels/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "int32/u64 (integer draw), i8 MFMA -> i32 pairs",
+        "data": "synthetic instance %s (tests/golden/instances), Philox seed %d" % (inst_dir, args.seed),
+        "config": {"workload": "%s: %d LEGACY panels/GPU/step, k=%d, n=%d, C=%d, F=%d, counts+%sunique" % (
+            args.config, S, k, n, enc.C, enc.F, "pairs+" if want_pairs else ""),
+            "panels_per_gpu_per_step": S, "instance": inst_dir, "parallelism": "panel shards x%d" % world},
+        "roofline": roof,
+        "kernels": kernels,
+    }
+    if want_pairs:
+        result["xtx_mfma_util"] = kernels["pairs_mfma"]["mfma_util"]
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cb = cpu_baseline(inst_dir, k, args.seed, args.cpu_seconds, want_pairs)
+        result["cpu_baseline"] = cb
+        result["speedup_vs_cpu"] = result["value"] / cb["value"]
+    elif rank == 0:
+        result["cpu_baseline"] = None
+    if rank == 0:
+        print(json.dumps(result))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,18 @@
+"""MI355X-native LEGACY Monte Carlo engine (citizens'-assembly replication hot path).
+
+The package directory name contains a hyphen, so import it with
+``importlib.import_module("citizensassemblies-replication_amd")`` (or add the
+directory to ``sys.path``).  Public surface, mirroring the
+reference's legacy.py / analysis.py LEGACY functions:
+
+    read_instance, Instance, PairHistogram, SelectionError, check_min_cats,
+    find_random_sample_legacy, legacy_find, legacy_probabilities, seed
+"""
+from .instance import Instance, read_instance, encode  # noqa: F401
+from .legacy import SelectionError, check_min_cats, find_random_sample_legacy, seed  # noqa: F401
+from .analysis import PairHistogram, PanelSet, legacy_find, legacy_find_batch, legacy_probabilities  # noqa: F401
+from . import _native  # noqa: F401
+
+__all__ = ["Instance", "read_instance", "encode", "SelectionError", "check_min_cats",
+           "find_random_sample_legacy", "seed", "PairHistogram", "PanelSet", "legacy_find",
+           "legacy_find_batch", "legacy_probabilities"]

@@ -1,0 +1,117 @@
+"""ctypes binding of libcsa_legacy.so (C ABI declared in include/csa_legacy.h).
+
+The library is built in-tree by :func:`build` (``hipcc --offload-arch=gfx950``).
+There is no fallback: if the library is missing or a call fails, the error is
+raised to the caller.
+"""
+import ctypes
+import os
+import subprocess
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
+LIB_PATH = os.path.join(HERE, "libcsa_legacy.so")
+SRC = os.path.join(HERE, "csrc", "csa_legacy.hip")
+HEADER = os.path.join(REPO, "include", "csa_legacy.h")
+
+CSA_OK = 0
+CSA_E_INVALID = 1
+CSA_E_BAD_QUOTAS = 2
+CSA_E_NO_CANDIDATE = 3
+CSA_E_ATTEMPT_LIMIT = 4
+CSA_E_UNSUPPORTED = 5
+CSA_E_HIP = 6
+CSA_E_SELECTION = 7
+
+CSA_WANT_PANELS = 0x1
+CSA_WANT_COUNTS = 0x2
+CSA_WANT_PAIRS = 0x4
+CSA_WANT_UNIQUE = 0x8
+
+# every symbol include/csa_legacy.h declares, with its ctypes signature
+_P = ctypes.c_void_p
+_I32 = ctypes.c_int32
+_U32 = ctypes.c_uint32
+_U64 = ctypes.c_uint64
+SIGNATURES = {
+    "csa_version": (ctypes.c_int, []),
+    "csa_last_error": (ctypes.c_char_p, []),
+    "csa_device_count": (ctypes.c_int, [_P]),
+    "csa_instance_create": (ctypes.c_int, [_I32, _I32, _I32, _P, _P, _P, _P, _P]),
+    "csa_instance_destroy": (None, [_P]),
+    "csa_instance_info": (ctypes.c_int, [_P, _P, _P, _P, _P]),
+    "csa_instance_set_state": (ctypes.c_int, [_P, _P, _P, _P]),
+    "csa_legacy_sample": (ctypes.c_int, [_P, _I32, _U64, _U64, _U64, _U32, _U32, _P, _P, _P, _P, _P]),
+    "csa_legacy_find": (ctypes.c_int, [_P, _I32, _U64, _U64, _U64, _U32, _P, _P]),
+    "csa_legacy_attempt": (ctypes.c_int, [_P, _I32, _U64, _U64, _U32, _P, _P, _P, _P, _P]),
+    "csa_draw_async": (ctypes.c_int, [_P, _I32, _U64, _U64, _U64, _U32, _P, _P, _P, _P, _P, _P]),
+    "csa_xt_pad": (_I32, [_I32]),
+    "csa_transpose_count_async": (ctypes.c_int, [_P, _U64, _I32, _P, _P, _P]),
+    "csa_pair_counts_async": (ctypes.c_int, [_P, _U64, _I32, _P, _P]),
+    "csa_unique_async": (ctypes.c_int, [_P, _P, _U64, _I32, _P, _U64, _P, _P]),
+    "csa_unique_hashes_async": (ctypes.c_int, [_P, _U64, _U32, _U32, _P, _U64, _P, _P]),
+    "csa_status_decode": (ctypes.c_int, [_P]),
+}
+
+_lib = None
+
+
+class NativeLibraryError(RuntimeError):
+    """libcsa_legacy.so is missing or failed to load (no CPU fallback exists)."""
+
+
+class CsaError(RuntimeError):
+    def __init__(self, code, message):
+        super().__init__("csa error %d: %s" % (code, message))
+        self.code = code
+
+
+def build(verbose=False):
+    """Compile csrc/csa_legacy.hip for gfx950 into LIB_PATH (in-tree)."""
+    cmd = ["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wall",
+           "-o", LIB_PATH, SRC]
+    if verbose:
+        print(" ".join(cmd))
+    subprocess.check_call(cmd)
+    return LIB_PATH
+
+
+def lib():
+    """Load (once) and return the ctypes library; raises NativeLibraryError if absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise NativeLibraryError(
+            "%s not found: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+            "(hipcc --offload-arch=gfx950); the LEGACY path has no CPU fallback" % LIB_PATH)
+    try:
+        L = ctypes.CDLL(LIB_PATH)
+    except OSError as e:
+        raise NativeLibraryError("failed to load %s: %s" % (LIB_PATH, e)) from e
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = L
+    return L
+
+
+def last_error():
+    msg = lib().csa_last_error()
+    return msg.decode("utf-8", "replace") if msg else ""
+
+
+def check(rc):
+    if rc != CSA_OK:
+        raise CsaError(rc, last_error())
+    return rc
+
+
+def ptr(a):
+    """Address of a numpy array / torch tensor (or None)."""
+    if a is None:
+        return None
+    if hasattr(a, "data_ptr"):
+        return ctypes.c_void_p(a.data_ptr())
+    return a.ctypes.data_as(ctypes.c_void_p)

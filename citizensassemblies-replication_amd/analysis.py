@@ -1,0 +1,213 @@
+"""Drop-in for the LEGACY part of the reference's analysis.py, backed by HIP kernels.
+
+Kept names and semantics (reference file:line):
+  * ``Instance``, ``read_instance``    analysis.py:54-58, 108-138 (from .instance)
+  * ``PairHistogram``                  analysis.py:68-98 -- same methods, backed by a
+                                       dense count matrix instead of an n(n-1)/2 dict
+  * ``legacy_find``                    analysis.py:141-159 -- restarts run on the device
+  * ``legacy_probabilities``           analysis.py:162-191 -- the batch entry point:
+                                       draw S panels (one per wavefront), per-person
+                                       counts, X^T X pair counts on int8 MFMA,
+                                       distinct-panel count; returns
+                                       ``(alloc, found_panels, pair_histogram)``.
+LEXIMIN / XMIN and the plotting / statistics code stay in the reference (CPU).
+"""
+import ctypes
+from typing import Dict, List, Tuple
+
+import numpy as np
+
+from . import _native as N
+from .instance import Instance, read_instance, encode, unpack_panel  # noqa: F401
+from .legacy import STREAM, seed, SelectionError, check_min_cats  # noqa: F401
+
+ProbAllocation = Dict
+
+
+class PairHistogram:
+    """analysis.py:68-98 with a dense backing store.
+
+    ``counts`` is an (n, n) array whose strict upper triangle holds the pair
+    values (row-major i < j is the reference's key order, analysis.py:70);
+    the lower triangle is ignored.  Integer counts stay exact until
+    ``turn_into_probabilities_by_dividing_all_elements_by_given_number``
+    divides them (float64 true division, as the reference's ``/``).
+    """
+
+    def __init__(self, number_of_agents, uniform_distribution=False, counts=None):
+        n = int(number_of_agents)
+        self.n = n
+        if counts is not None:
+            self._m = np.asarray(counts)
+            assert self._m.shape == (n, n)
+        else:
+            self._m = np.zeros((n, n), np.int64)
+        if uniform_distribution:
+            npairs = n * (n - 1) // 2
+            self._m = np.full((n, n), 1 / npairs if npairs else 0.0, np.float64)
+
+    # dict-compatible accessors -----------------------------------------------------------
+    def _key(self, key):
+        i, j = sorted(key)
+        if not (0 <= i < j < self.n):
+            raise KeyError(key)
+        return i, j
+
+    def __getitem__(self, key):
+        i, j = self._key(key)
+        v = self._m[i, j]
+        return v.item()
+
+    def __setitem__(self, key, value):
+        i, j = self._key(key)
+        if isinstance(value, float) and self._m.dtype.kind != "f":
+            self._m = self._m.astype(np.float64)
+        self._m[i, j] = value
+
+    def turn_into_probabilities_by_dividing_all_elements_by_given_number(self, num):
+        self._m = self._m / num
+
+    def add_portfolio_of_panels_to_histogram(self, portfolio, probabilities):
+        for panel, pob in zip(portfolio, probabilities):
+            idx = np.asarray(sorted(panel), np.int64)
+            if isinstance(pob, float) and self._m.dtype.kind != "f":
+                self._m = self._m.astype(np.float64)
+            ii, jj = np.triu_indices(len(idx), 1)
+            np.add.at(self._m, (idx[ii], idx[jj]), pob)
+
+    def upper(self):
+        """Values of all pairs i < j in the reference's key order (row-major)."""
+        return self._m[np.triu_indices(self.n, 1)]
+
+    def get_dict(self):
+        iu = np.triu_indices(self.n, 1)
+        vals = self._m[iu].tolist()
+        return dict(zip(zip(iu[0].tolist(), iu[1].tolist()), vals))
+
+    def __len__(self):
+        return self.n * (self.n - 1) // 2
+
+    def __getstate__(self):
+        return {"n": self.n, "m": self._m}
+
+    def __setstate__(self, st):
+        self.n, self._m = st["n"], st["m"]
+
+
+class PanelSet:
+    """Set of distinct panels (found_panels, analysis.py:171,186), lazily materialised.
+
+    ``len()`` is the device's distinct-panel count; iteration / membership
+    decode the packed bitmasks (sorted agent-id tuples, as the reference).
+    """
+
+    def __init__(self, unique_count, packed=None, n=0, agent_ids=None):
+        self._count = int(unique_count)
+        self._packed = packed
+        self._n = n
+        self._ids = agent_ids
+        self._set = None
+
+    def __len__(self):
+        return self._count
+
+    def _materialise(self):
+        if self._set is None:
+            if self._packed is None:
+                raise RuntimeError("panels were not kept; only len() is available")
+            rows = np.unique(np.ascontiguousarray(self._packed), axis=0)
+            ids = self._ids
+            self._set = {tuple(ids[p] for p in unpack_panel(r, self._n)) for r in rows}
+        return self._set
+
+    def __iter__(self):
+        return iter(self._materialise())
+
+    def __contains__(self, panel):
+        return tuple(panel) in self._materialise()
+
+    def __eq__(self, other):
+        return set(self) == set(other)
+
+
+def legacy_find(feature_info, agents, k) -> List:
+    """analysis.py:141-159: one accepted panel, pick order, restarts on the device."""
+    enc = encode(feature_info, agents)
+    k = int(k)
+    picks = np.full(max(k, 1), -1, np.int32)
+    first = STREAM.take_panels(1)
+    N.check(N.lib().csa_legacy_find(enc.handle, k, STREAM.key, first, 1, 0, N.ptr(picks), None))
+    return [enc.agent_ids[int(p)] for p in picks[:k] if p >= 0]
+
+
+def legacy_find_batch(feature_info, agents, k, count, max_attempts=0):
+    """``count`` consecutive legacy_find calls in one launch (XMIN's caller, xmin.py:464-474)."""
+    enc = encode(feature_info, agents)
+    k = int(k)
+    picks = np.full((int(count), max(k, 1)), -1, np.int32)
+    first = STREAM.take_panels(count)
+    N.check(N.lib().csa_legacy_find(enc.handle, k, STREAM.key, first, int(count), max_attempts,
+                                    N.ptr(picks), None))
+    ids = enc.agent_ids
+    return [[ids[int(p)] for p in row[:k] if p >= 0] for row in picks]
+
+
+class LegacyRaw:
+    """Integer results of one legacy_probabilities run (exact, before division)."""
+
+    def __init__(self, counts, pairs, unique, panels, attempts):
+        self.counts, self.pairs, self.unique, self.panels, self.attempts = counts, pairs, unique, panels, attempts
+
+
+def legacy_sample_raw(enc, k, iterations, random_seed, panel_begin=0, want_pairs=True, want_panels=True,
+                      want_attempts=False, max_attempts=0):
+    """Run the whole batch through csa_legacy_sample and return integer results."""
+    S = int(iterations)
+    flags = N.CSA_WANT_COUNTS | N.CSA_WANT_UNIQUE
+    counts = np.zeros(enc.n, np.int64)
+    pairs = np.zeros((enc.n, enc.n), np.int64) if want_pairs else None
+    panels = np.zeros((S, enc.W), np.uint64) if want_panels else None
+    attempts = np.zeros(S, np.uint32) if want_attempts else None
+    unique = np.zeros(1, np.uint64)
+    if want_pairs:
+        flags |= N.CSA_WANT_PAIRS
+    if want_panels:
+        flags |= N.CSA_WANT_PANELS
+    rc = N.lib().csa_legacy_sample(enc.handle, int(k), int(random_seed) & 0xFFFFFFFFFFFFFFFF, panel_begin, S, flags,
+                                   max_attempts, N.ptr(panels), N.ptr(counts), N.ptr(pairs), N.ptr(unique),
+                                   N.ptr(attempts))
+    if rc == N.CSA_E_BAD_QUOTAS:
+        raise AssertionError(N.last_error())     # analysis.py:174-176
+    if rc == N.CSA_E_NO_CANDIDATE:
+        raise KeyError("")                       # legacy.py:188
+    N.check(rc)
+    return LegacyRaw(counts, pairs, int(unique[0]), panels, attempts)
+
+
+def legacy_probabilities(instance: Instance, iterations: int, random_seed: int,
+                         keep_panels: bool = True) -> Tuple[ProbAllocation, PanelSet, PairHistogram]:
+    """analysis.py:162-191 on the GPU.
+
+    Returns ``({agent_id: count/S}, found_panels, pair_histogram)`` with the
+    pair histogram already divided by S, as the reference.  With
+    torch.distributed initialised and world size > 1 the panels are sharded
+    over ranks (see ``distributed.legacy_probabilities_distributed``).
+    """
+    from . import distributed as D
+    if D.world_size() > 1:
+        return D.legacy_probabilities_distributed(instance, iterations, random_seed, keep_panels=keep_panels)
+    seed(random_seed)
+    enc = encode(instance.categories, instance.agents)
+    enc.check_quotas(instance.k)
+    S = int(iterations)
+    STREAM.take_panels(S)
+    raw = legacy_sample_raw(enc, instance.k, S, random_seed, want_pairs=True, want_panels=keep_panels)
+    return finish(instance, enc, raw, S)
+
+
+def finish(instance, enc, raw, S):
+    alloc = {aid: int(raw.counts[p]) / S for p, aid in enumerate(enc.agent_ids)}
+    hist = PairHistogram(len(instance.agents), counts=raw.pairs)
+    hist.turn_into_probabilities_by_dividing_all_elements_by_given_number(S)
+    panels = PanelSet(raw.unique, raw.panels, enc.n, enc.agent_ids)
+    return alloc, panels, hist

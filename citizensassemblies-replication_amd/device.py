@@ -1,0 +1,110 @@
+"""Device-resident LEGACY pipeline on one GPU (stream-ordered C ABI + torch buffers).
+
+PyTorch only provides device memory, the stream and (in distributed.py) the
+RCCL collectives; every kernel is the hand-written HIP in csrc/.  One
+``run`` = one pass of analysis.py:162-191 over a shard of panels:
+
+    draw_kernel        panels [panel_begin, panel_begin+S) -> packed bitmasks + 128-bit hashes
+    xt_count_kernel    bitmasks -> transposed panel-indicator bits + per-person counts (+=)
+    pair_mfma_kernel   transposed bits -> pair counts X^T X (+=)        (if want_pairs)
+    unique_kernel      hashes (+ bitmasks) -> distinct-panel count (+=)  (if want_unique)
+
+Buffers are allocated once for the largest shard and reused across runs, so a
+timed loop measures kernels only.
+"""
+import ctypes
+
+import torch
+
+from . import _native as N
+
+
+def _stream_ptr(stream):
+    return ctypes.c_void_p(stream.cuda_stream) if stream is not None else None
+
+
+class DevicePipeline:
+    def __init__(self, enc, k, max_panels, want_pairs=True, want_unique=True, want_attempts=False,
+                 device=None, stream=None):
+        self.enc = enc
+        self.k = int(k)
+        self.device = torch.device(device or "cuda")
+        self.stream = stream or torch.cuda.current_stream(self.device)
+        self.want_pairs = want_pairs
+        self.want_unique = want_unique
+        S = int(max_panels)
+        self.max_panels = S
+        n, W = enc.n, enc.W
+        L = N.lib()
+        self.npad = int(L.csa_xt_pad(max(n, 1)))
+        nblk = (S + 63) // 64
+        slots = 1
+        while slots < max(2 * S, 64):
+            slots <<= 1
+        self.slots = slots
+        dev = self.device
+        u64 = torch.int64  # raw 64-bit words; reinterpretation is done by the kernels
+        with torch.cuda.device(dev):
+            self.panels = torch.empty(S * W, dtype=u64, device=dev)
+            self.hashes = torch.empty(2 * S, dtype=u64, device=dev) if want_unique else None
+            self.attempts = torch.empty(S, dtype=torch.int32, device=dev) if want_attempts else None
+            self.status = torch.zeros(4, dtype=torch.int32, device=dev)
+            self.counts = torch.zeros(n, dtype=torch.int64, device=dev)
+            self.xt = torch.empty(nblk * self.npad, dtype=u64, device=dev) if want_pairs else None
+            self.pairs = torch.zeros(n * n, dtype=torch.int64, device=dev) if want_pairs else None
+            self.table = torch.empty(slots, dtype=u64, device=dev) if want_unique else None
+            self.unique = torch.zeros(1, dtype=torch.int64, device=dev)
+        _ = enc.handle  # upload the instance on this device
+
+    def reset(self):
+        with torch.cuda.stream(self.stream):
+            self.status.zero_()
+            self.counts.zero_()
+            self.unique.zero_()
+            if self.pairs is not None:
+                self.pairs.zero_()
+
+    # individual stages (stream-ordered, no sync) -------------------------------------------
+    def draw(self, seed, panel_begin, S, max_attempts=0):
+        assert S <= self.max_panels
+        N.check(N.lib().csa_draw_async(self.enc.handle, self.k, int(seed) & 0xFFFFFFFFFFFFFFFF, int(panel_begin),
+                                       int(S), max_attempts, N.ptr(self.panels), N.ptr(self.hashes),
+                                       N.ptr(self.attempts), None, N.ptr(self.status),
+                                       _stream_ptr(self.stream)))
+
+    def transpose_count(self, S):
+        N.check(N.lib().csa_transpose_count_async(N.ptr(self.panels), int(S), self.enc.n,
+                                                  N.ptr(self.xt) if self.want_pairs else None,
+                                                  N.ptr(self.counts), _stream_ptr(self.stream)))
+
+    def pair_counts(self, S):
+        N.check(N.lib().csa_pair_counts_async(N.ptr(self.xt), (int(S) + 63) // 64, self.enc.n,
+                                              N.ptr(self.pairs), _stream_ptr(self.stream)))
+
+    def unique_count(self, S):
+        N.check(N.lib().csa_unique_async(N.ptr(self.hashes), N.ptr(self.panels), int(S), self.enc.W,
+                                         N.ptr(self.table), self.slots, N.ptr(self.unique),
+                                         _stream_ptr(self.stream)))
+
+    def run(self, seed, panel_begin, S, max_attempts=0):
+        """Enqueue the whole pass; results accumulate into counts / pairs / unique."""
+        self.draw(seed, panel_begin, S, max_attempts)
+        self.transpose_count(S)
+        if self.want_pairs:
+            self.pair_counts(S)
+        if self.want_unique:
+            self.unique_count(S)
+
+    def check_status(self):
+        """Synchronise and raise on a device-side error (no-candidate, attempt limit)."""
+        self.stream.synchronize()
+        h = self.status.cpu().numpy().astype("uint32")
+        rc = N.lib().csa_status_decode(N.ptr(h))
+        if rc == N.CSA_E_NO_CANDIDATE:
+            raise KeyError("")       # legacy.py:188
+        N.check(rc)
+
+    def panels_view(self, S):
+        """Host copy of the packed panels (uint64[S, W])."""
+        import numpy as np
+        return self.panels[: S * self.enc.W].cpu().numpy().view(np.uint64).reshape(S, self.enc.W)

@@ -1,0 +1,164 @@
+/*
+ * csa_legacy.h -- C ABI of the MI355X-native LEGACY Monte Carlo engine
+ * (libcsa_legacy.so, built from citizensassemblies-replication_amd/csrc/).
+ *
+ * The reference (sirandreww/citizensassemblies-replication) has no FFI: its
+ * boundary is a Python call surface.  Each entry point below names the
+ * reference function it replaces (file:line); the Python mirror in
+ * citizensassemblies-replication_amd/{legacy,analysis}.py binds them through
+ * ctypes and keeps the reference signatures.  INTEGRATION.md shows the
+ * binding a maintainer adds to the reference.
+ *
+ * Conventions
+ *   - plain C types only; the caller owns every buffer; no exception crosses
+ *     the ABI; every function returns a CSA_* status code (0 = ok) and leaves
+ *     a thread-local message in csa_last_error().
+ *   - an instance lives on the HIP device that was current when it was
+ *     created (one process per GPU; multi-GPU sharding and the RCCL
+ *     all-reduce live in the Python layer, see DESIGN.md "Multi-GPU").
+ *   - agent ids are 0..n-1 = pool row order (analysis.py:131-133); feature
+ *     ids are 0..F-1 in category-major CSV order (analysis.py:114-124).
+ *   - randomness: Philox4x32-10 verification-mode stream, keyed by
+ *     (seed, panel, attempt, step) -- see oracle/philox.py for the contract.
+ *   - bitmask panels: uint64 words, W = ceil(n/64) per panel, agent p is
+ *     bit (p & 63) of word (p >> 6).
+ */
+#ifndef CSA_LEGACY_H
+#define CSA_LEGACY_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes --------------------------------------------------------- */
+#define CSA_OK 0
+#define CSA_E_INVALID 1        /* bad argument / inconsistent instance                         */
+#define CSA_E_BAD_QUOTAS 2     /* sum(min) <= k <= sum(max) violated: analysis.py:174-176 assert */
+#define CSA_E_NO_CANDIDATE 3   /* no candidate feature: the reference's KeyError, legacy.py:188  */
+#define CSA_E_ATTEMPT_LIMIT 4  /* new: the reference restarts forever (analysis.py:146)          */
+#define CSA_E_UNSUPPORTED 5    /* instance exceeds the kernels' limits (F > 64, n > 16384, ...)  */
+#define CSA_E_HIP 6            /* HIP runtime / device error                                     */
+#define CSA_E_SELECTION 7      /* one attempt raised SelectionError (legacy.py:34-36)            */
+
+/* ---- flags for csa_legacy_sample ----------------------------------------- */
+#define CSA_WANT_PANELS 0x1u   /* copy packed panels (n_panels * W uint64) to panels_out   */
+#define CSA_WANT_COUNTS 0x2u   /* per-person counts (analysis.py:179,187)                  */
+#define CSA_WANT_PAIRS 0x4u    /* pair co-selection counts (PairHistogram, analysis.py:68) */
+#define CSA_WANT_UNIQUE 0x8u   /* number of distinct panels (found_panels, analysis.py:171) */
+
+typedef struct csa_instance csa_instance;
+
+int csa_version(void);                 /* ABI version, currently 1 */
+const char *csa_last_error(void);      /* thread-local message of the last failing call */
+int csa_device_count(int32_t *out);    /* HIP devices visible to this process */
+
+/* Encode an instance (replaces read_instance's dicts, analysis.py:108-138).
+ * person_feat: n*C global feature ids (row p = agent p, column c = category c);
+ * fmin/fmax: F quotas; feat_cat: F category ids (features of one category are
+ * contiguous, category-major).  Uploads the feature bitmasks to the current
+ * device.  Initial state: selected = 0, remaining = pool counts, all present. */
+int csa_instance_create(int32_t n, int32_t C, int32_t F, const int32_t *person_feat,
+                        const int32_t *fmin, const int32_t *fmax, const int32_t *feat_cat,
+                        csa_instance **out);
+void csa_instance_destroy(csa_instance *inst);
+/* n, C, F, W = ceil(n/64) */
+int csa_instance_info(const csa_instance *inst, int32_t *n, int32_t *C, int32_t *F, int32_t *W);
+/* Replace the initial draw state (for find_random_sample_legacy called on
+ * partially used dicts): sel/rem: F counters ("selected"/"remaining" of
+ * legacy.py's category items), present: W words of the people dict's keys.
+ * Any NULL argument restores that part of the default state. */
+int csa_instance_set_state(csa_instance *inst, const int32_t *sel, const int32_t *rem,
+                           const uint64_t *present);
+
+/* ---- host-buffer API (blocking) ------------------------------------------ */
+
+/* legacy_probabilities (analysis.py:162-191) for panels
+ * [panel_begin, panel_begin + n_panels): draw every panel with restarts
+ * (legacy_find, analysis.py:141-159), then reduce.  Outputs (host memory,
+ * each may be NULL when its flag is clear):
+ *   panels_out    n_panels * W uint64, panel order            (CSA_WANT_PANELS)
+ *   person_counts n int64                                      (CSA_WANT_COUNTS)
+ *   pair_counts   n * n int64, row-major; entries i < j and the
+ *                 diagonal (= person_counts) are valid; the rest
+ *                 is unspecified                               (CSA_WANT_PAIRS)
+ *   unique_out    1 uint64 = number of distinct panels          (CSA_WANT_UNIQUE)
+ *   attempts_out  n_panels uint32 attempts used per panel (>= 1), or NULL
+ * max_attempts caps restarts per panel (0 = default 100000). */
+int csa_legacy_sample(csa_instance *inst, int32_t k, uint64_t seed, uint64_t panel_begin,
+                      uint64_t n_panels, uint32_t flags, uint32_t max_attempts,
+                      uint64_t *panels_out, int64_t *person_counts, int64_t *pair_counts,
+                      uint64_t *unique_out, uint32_t *attempts_out);
+
+/* legacy_find (analysis.py:141-159), batched: panels in pick order.
+ * picks_out: n_panels * k int32 (a step that picked nobody -- only possible
+ * with an inconsistent initial state -- is -1); attempts_out may be NULL. */
+int csa_legacy_find(csa_instance *inst, int32_t k, uint64_t seed, uint64_t panel_begin,
+                    uint64_t n_panels, uint32_t max_attempts, int32_t *picks_out,
+                    uint32_t *attempts_out);
+
+/* One call of find_random_sample_legacy (legacy.py:178-200) = one attempt
+ * (seed, panel, attempt) from the instance's initial state.  Returns CSA_OK
+ * (picks + final state written), CSA_E_SELECTION (SelectionError; state
+ * outputs unspecified) or CSA_E_NO_CANDIDATE.  picks_out: k int32 in pick
+ * order, *n_picks set; sel_out/rem_out: F; present_out: W (any may be NULL). */
+int csa_legacy_attempt(csa_instance *inst, int32_t k, uint64_t seed, uint64_t panel,
+                       uint32_t attempt, int32_t *picks_out, int32_t *n_picks, int32_t *sel_out,
+                       int32_t *rem_out, uint64_t *present_out);
+
+/* ---- stream-ordered device API ---------------------------------------------
+ * All buffers are device pointers on the instance's device; `stream` is a
+ * hipStream_t (NULL = default stream).  Nothing synchronises; errors inside
+ * kernels land in d_status (4 uint32: code, panel lo, panel hi, last attempt
+ * result) which the caller zeroes before the first launch and decodes with
+ * csa_status_decode after synchronising. */
+
+/* Draw kernel: one panel per wavefront, LDS-resident feature bitmasks.
+ * d_panels: n_panels*W (required); d_hashes: 2*n_panels 128-bit panel hashes
+ * (or NULL); d_attempts: n_panels (or NULL); d_picks: n_panels*k (or NULL). */
+int csa_draw_async(const csa_instance *inst, int32_t k, uint64_t seed, uint64_t panel_begin,
+                   uint64_t n_panels, uint32_t max_attempts, uint64_t *d_panels,
+                   uint64_t *d_hashes, uint32_t *d_attempts, int32_t *d_picks,
+                   uint32_t *d_status, void *stream);
+
+/* Bit-transpose + per-person count.  Panels (n_panels*W) -> d_xt, the
+ * panel-indicator matrix transposed and packed: d_xt[b * n_pad + p] holds
+ * bits of agent p for panels 64b..64b+63; n_pad = csa_xt_pad(n), blocks
+ * b < ceil(n_panels/64).  d_counts (n int64) is ACCUMULATED (+=); d_xt may be
+ * NULL (counts only). */
+int32_t csa_xt_pad(int32_t n);
+int csa_transpose_count_async(const uint64_t *d_panels, uint64_t n_panels, int32_t n,
+                              uint64_t *d_xt, int64_t *d_counts, void *stream);
+
+/* Pair counts X^T X on int8 MFMA (v_mfma_i32_32x32x32_i8), upper-triangular
+ * tiles, split over panel blocks.  d_xt as produced above (n_blocks =
+ * ceil(n_panels/64)); d_pairs (n*n int64, row-major) is ACCUMULATED (+=) for
+ * i <= j (lower triangle unspecified).  Exact for n_panels < 2^31 per call. */
+int csa_pair_counts_async(const uint64_t *d_xt, uint64_t n_blocks, int32_t n, int64_t *d_pairs,
+                          void *stream);
+
+/* Distinct-panel count: open-addressing table of panel indices keyed by the
+ * 128-bit hashes, with full-bitmask comparison when d_panels != NULL (exact).
+ * d_table: table_slots uint64 (power of two >= 2*n_panels), zeroed by the
+ * call; *d_unique (uint64) is ACCUMULATED. */
+int csa_unique_async(const uint64_t *d_hashes, const uint64_t *d_panels, uint64_t n_panels,
+                     int32_t W, uint64_t *d_table, uint64_t table_slots, uint64_t *d_unique,
+                     void *stream);
+
+/* Multi-GPU distinct-panel step: insert the 128-bit hashes (2*n_hashes
+ * uint64, e.g. every rank's hashes after an all-gather) whose owner
+ * h1 % world equals `rank`, comparing hashes only; *d_unique is ACCUMULATED.
+ * Summing the per-rank results (all-reduce) gives the global count. */
+int csa_unique_hashes_async(const uint64_t *d_hashes, uint64_t n_hashes, uint32_t world, uint32_t rank,
+                            uint64_t *d_table, uint64_t table_slots, uint64_t *d_unique, void *stream);
+
+/* Decode a device status block (host copy of the 4 words) into a CSA_* code
+ * and set csa_last_error() accordingly. */
+int csa_status_decode(const uint32_t *h_status);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CSA_LEGACY_H */

@@ -1,0 +1,214 @@
+"""GPU parity: the HIP path (through the C ABI) vs the reference goldens and the C oracle.
+
+Bar: panels, attempts, per-person counts, pair counts and distinct-panel counts
+bit-exact; derived probabilities equal to the reference's floats (count / S is
+correctly rounded on both sides, so the 1e-12 tolerance of the north star is
+met with equality).
+"""
+import ctypes
+import hashlib
+
+import numpy as np
+import pytest
+
+from conftest import PHILOX_CASES, golden, inst_paths, pkg
+from oracle import coracle
+from oracle.legacy_oracle import read_instance as oracle_read, draw_attempt, PhiloxRng, FAIL, NoCandidateError
+
+pytestmark = pytest.mark.gpu
+
+
+def _sha(a):
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+def _enc(name, k):
+    P = pkg()
+    inst = P.read_instance(*inst_paths(name), k)
+    return inst, P.encode(inst.categories, inst.agents)
+
+
+@pytest.mark.parametrize("case", PHILOX_CASES)
+def test_sample_matches_reference_golden(gpu_available, case):
+    A = pkg("analysis")
+    g = golden(case)
+    inst, enc = _enc(g["instance"], g["k"])
+    raw = A.legacy_sample_raw(enc, g["k"], g["S"], g["seed"], want_pairs=True, want_panels=True,
+                              want_attempts=True)
+    assert _sha(raw.panels) == g["panels_sha256"]
+    assert raw.attempts.tolist() == g["attempts"]
+    assert raw.counts.tolist() == g["counts"]
+    assert raw.unique == g["unique"]
+    up = raw.pairs[np.triu_indices(enc.n, 1)]
+    assert _sha(up) == g["pair_upper_sha256"]
+    assert np.array_equal(np.diag(raw.pairs), raw.counts)
+    assert _sha(up / g["S"]) == g["pair_prob_sha256"]        # the reference's float64 pair values
+
+
+@pytest.mark.parametrize("case", ["couples_s0", "example_small_20_s0", "sf_e_tight_110_s1", "pathological_5_s0"])
+def test_legacy_find_pick_order(gpu_available, case):
+    A = pkg("analysis")
+    g = golden(case)
+    inst, _ = _enc(g["instance"], g["k"])
+    A.seed(g["seed"])
+    batch = A.legacy_find_batch(inst.categories, inst.agents, g["k"], len(g["first_picks"]))
+    assert batch == g["first_picks"]
+    A.seed(g["seed"])
+    one = [A.legacy_find(inst.categories, inst.agents, g["k"]) for _ in range(4)]
+    assert one == g["first_picks"][:4]
+
+
+def test_legacy_probabilities_api(gpu_available):
+    A = pkg("analysis")
+    g = golden("example_small_20_s0")
+    inst, _ = _enc(g["instance"], g["k"])
+    alloc, found, hist = A.legacy_probabilities(inst, g["S"], g["seed"])
+    assert [alloc[i] for i in range(len(alloc))] == g["alloc"]
+    assert len(found) == g["unique"]
+    assert tuple(g["first_panels"][0]) in found
+    up = hist.upper()
+    assert up.tolist() == (np.asarray(g["pair_upper"]) / g["S"]).tolist()
+    assert hist[(5, 3)] == hist[(3, 5)]
+
+
+@pytest.mark.parametrize("name,k,S,seed", [("sf_e_110", 110, 20000, 7), ("sf_e_tight_110", 110, 5000, 3),
+                                           ("example_large_200", 200, 4000, 11),
+                                           ("synthetic8192_200", 200, 600, 5), ("rejecty_6", 6, 50000, 9)])
+def test_sample_matches_c_oracle(gpu_available, name, k, S, seed):
+    A = pkg("analysis")
+    inst, enc = _enc(name, k)
+    begin = 123456789          # non-zero panel_begin: sharded runs start mid-stream
+    N = pkg("_native")
+    counts = np.zeros(enc.n, np.int64)
+    pairs = np.zeros((enc.n, enc.n), np.int64)
+    panels = np.zeros((S, enc.W), np.uint64)
+    attempts = np.zeros(S, np.uint32)
+    uniq = np.zeros(1, np.uint64)
+    flags = N.CSA_WANT_PANELS | N.CSA_WANT_COUNTS | N.CSA_WANT_PAIRS | N.CSA_WANT_UNIQUE
+    N.check(N.lib().csa_legacy_sample(enc.handle, k, seed, begin, S, flags, 0, N.ptr(panels), N.ptr(counts),
+                                      N.ptr(pairs), N.ptr(uniq), N.ptr(attempts)))
+    o = oracle_read(*inst_paths(name), k)
+    rc, opanels, oatt, _ = coracle.draw(o, k, seed, begin, S)
+    assert rc == 0
+    assert np.array_equal(panels, opanels)
+    assert np.array_equal(attempts, oatt)
+    assert np.array_equal(counts, coracle.counts(opanels, enc.n))
+    assert int(uniq[0]) == coracle.unique(opanels, enc.n)
+    if enc.n <= 2000:
+        op = coracle.pairs(opanels, enc.n)
+        iu = np.triu_indices(enc.n, 1)
+        assert np.array_equal(pairs[iu], op[iu])
+    assert np.array_equal(np.diag(pairs), counts)
+
+
+def test_full_size_properties_sf_e(gpu_available):
+    """BASELINE config 2 size (10^6 panels): size-independent invariants + a sampled oracle check."""
+    A = pkg("analysis")
+    inst, enc = _enc("sf_e_110", 110)
+    S, k = 10 ** 6, 110
+    raw = A.legacy_sample_raw(enc, k, S, 0, want_pairs=True, want_panels=True, want_attempts=True)
+    assert int(raw.counts.sum()) == k * S
+    pc = np.unpackbits(raw.panels.view(np.uint8), axis=1).sum(axis=1)
+    assert (pc == k).all()
+    # row sums of the symmetric pair matrix = (k - 1) * counts
+    iu = np.triu_indices(enc.n, 1)
+    full = np.zeros_like(raw.pairs)
+    full[iu] = raw.pairs[iu]
+    full = full + full.T
+    assert np.array_equal(full.sum(axis=1), (k - 1) * raw.counts)
+    assert np.array_equal(np.diag(raw.pairs), raw.counts)
+    assert raw.unique <= S
+    # spot-check three windows of the stream against the oracle
+    o = oracle_read(*inst_paths("sf_e_110"), k)
+    for begin in (0, 500000, S - 2000):
+        rc, opanels, oatt, _ = coracle.draw(o, k, 0, begin, 2000)
+        assert np.array_equal(raw.panels[begin:begin + 2000], opanels)
+        assert np.array_equal(raw.attempts[begin:begin + 2000], oatt)
+
+
+def test_find_random_sample_legacy_single_attempts(gpu_available):
+    """legacy.py:178-200 surface: dict mutation + SelectionError, vs the oracle's draw_attempt."""
+    import copy
+    P = pkg()
+    L = pkg("legacy")
+    name, k = "pathological_5", 5
+    inst = P.read_instance(*inst_paths(name), k)
+    o = oracle_read(*inst_paths(name), k)
+    src = PhiloxRng(4)
+    L.seed(4)
+    n_ok = n_fail = 0
+    for attempt in range(40):
+        cats = copy.deepcopy(inst.categories)
+        people = copy.deepcopy(inst.agents)
+        status, picks, sel, rem, present = draw_attempt(o, k, src.for_attempt(0, attempt))
+        if status == FAIL:
+            with pytest.raises(L.SelectionError):
+                L.find_random_sample_legacy(cats, people, {}, k, False, [])
+            n_fail += 1
+            continue
+        selected, lines = L.find_random_sample_legacy(cats, people, {}, k, False, [])
+        n_ok += 1
+        assert list(selected) == picks
+        assert sorted(people) == [p for p in range(o.n) if present[p]]
+        flat = [cats[c][f] for c in cats for f in cats[c]]
+        assert [it["selected"] for it in flat] == sel
+        assert [it["remaining"] for it in flat] == rem
+    assert n_ok and n_fail
+
+
+def test_no_candidate_raises_keyerror(gpu_available):
+    """n=k=102, one feature with min 0: at step 101 ratio = -101 <= -100 -> KeyError (legacy.py:188)."""
+    P = pkg()
+    A = pkg("analysis")
+    cats = {"c": {"f": {"min": 0, "max": 200, "selected": 0, "remaining": 102}}}
+    agents = {i: {"c": "f"} for i in range(102)}
+    inst = P.Instance(k=102, categories=cats, agents=agents)
+    from oracle.legacy_oracle import OracleInstance
+    o = OracleInstance(k=102, cat_names=["c"], feat_names=[("c", "f")], fmin=[0], fmax=[200], fcat=[0],
+                       person_feat=[[0]] * 102)
+    with pytest.raises(NoCandidateError):
+        draw_attempt(o, 102, PhiloxRng(0).for_attempt(0, 0))
+    with pytest.raises(KeyError):
+        A.legacy_probabilities(inst, 10, 0)
+
+
+def test_attempt_limit_and_bad_quotas(gpu_available):
+    P = pkg()
+    N = pkg("_native")
+    A = pkg("analysis")
+    # infeasible: needs 2 x0 and 2 y0 with k=2 but nobody holds both -> every attempt fails
+    cats = {"x": {"x0": {"min": 2, "max": 2}, "x1": {"min": 0, "max": 2}},
+            "y": {"y0": {"min": 2, "max": 2}, "y1": {"min": 0, "max": 2}}}
+    agents = {0: {"x": "x0", "y": "y1"}, 1: {"x": "x0", "y": "y1"}, 2: {"x": "x1", "y": "y0"},
+              3: {"x": "x1", "y": "y0"}}
+    enc = P.encode(cats, agents)
+    with pytest.raises(N.CsaError) as ei:
+        A.legacy_sample_raw(enc, 2, 8, 0, want_pairs=False, want_panels=False, max_attempts=64)
+    assert ei.value.code == N.CSA_E_ATTEMPT_LIMIT
+    with pytest.raises(AssertionError):
+        A.legacy_sample_raw(enc, 7, 8, 0)          # sum(max) = 4 < 7 (analysis.py:176)
+
+
+def test_device_pipeline_matches_host_api(gpu_available):
+    """The stream-ordered path used by bench.py / distributed.py == csa_legacy_sample."""
+    import torch
+    A = pkg("analysis")
+    D = pkg("device")
+    inst, enc = _enc("sf_e_110", 110)
+    S = 30000
+    raw = A.legacy_sample_raw(enc, 110, S, 2, want_pairs=True, want_panels=True)
+    pipe = D.DevicePipeline(enc, 110, S)
+    pipe.reset()
+    # two shards through the same buffers: [0, S/2) and [S/2, S) accumulate
+    half = S // 2
+    pipe.run(2, 0, half)
+    pipe.check_status()
+    p0 = pipe.panels_view(half).copy()
+    pipe.run(2, half, S - half)
+    pipe.check_status()
+    p1 = pipe.panels_view(S - half)
+    assert np.array_equal(np.concatenate([p0, p1]), raw.panels)
+    assert np.array_equal(pipe.counts.cpu().numpy(), raw.counts)
+    iu = np.triu_indices(enc.n, 1)
+    assert np.array_equal(pipe.pairs.cpu().numpy().reshape(enc.n, enc.n)[iu], raw.pairs[iu])
+    torch.cuda.synchronize()
