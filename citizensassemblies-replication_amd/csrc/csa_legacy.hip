@@ -17,6 +17,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
@@ -46,7 +47,6 @@ int fail(int code, const char *fmt, ...) {
             return fail(CSA_E_HIP, "%s failed: %s", #expr, hipGetErrorString(e_));          \
     } while (0)
 
-constexpr int kWave = 64;
 constexpr int kDrawThreads = 256;
 constexpr uint32_t kDefaultMaxAttempts = 100000;
 
@@ -69,12 +69,6 @@ __device__ __forceinline__ void philox4x32_10(uint32_t &c0, uint32_t &c1, uint32
         c2 = n2;
         c3 = lo0;
     }
-}
-
-__device__ __forceinline__ uint64_t readlane64(uint64_t v, int lane) {
-    const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)v, lane);
-    const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(v >> 32), lane);
-    return ((uint64_t)hi << 32) | lo;
 }
 
 // position (0..63) of the rr-th (1-based) set bit of m; requires 1 <= rr <= popcount(m)
@@ -127,7 +121,96 @@ struct DrawArgs {
     uint64_t *present_out;
 };
 
-enum : int { kAccept = 0, kFail = 1, kReject = 2, kNoCandidate = 3 };
+// ---- sub-wave group primitives ------------------------------------------------------------
+// A panel is drawn by a group of G lanes (G = 16: one DPP row; 32; 64 = whole wave).  All
+// cross-lane traffic inside a group is DPP (quad_perm / row mirrors / row_shr / row_bcast)
+// except the xor-16 / xor-32 butterfly levels of G = 32 / 64 (ds_bpermute).
+constexpr int kNone = 1 << 24;  // "no candidate" feature index
+
+template <int CTRL, int ROW_MASK = 0xF, bool BOUND_ZERO = false>
+__device__ __forceinline__ int dpp(int old, int v) {
+    return __builtin_amdgcn_update_dpp(old, v, CTRL, ROW_MASK, 0xF, BOUND_ZERO);
+}
+
+// butterfly partner at level LVL: quad xor1, quad xor2, half-row mirror, row mirror, xor16, xor32
+template <int LVL>
+__device__ __forceinline__ int partner(int v) {
+    if constexpr (LVL == 0) return dpp<0xB1>(v, v);
+    else if constexpr (LVL == 1) return dpp<0x4E>(v, v);
+    else if constexpr (LVL == 2) return dpp<0x141>(v, v);
+    else if constexpr (LVL == 3) return dpp<0x140>(v, v);
+    else if constexpr (LVL == 4) return __shfl_xor(v, 16);
+    else return __shfl_xor(v, 32);
+}
+
+template <int LVL>
+__device__ __forceinline__ uint64_t partner64(uint64_t v) {
+    const uint32_t lo = (uint32_t)partner<LVL>((int)(uint32_t)v);
+    const uint32_t hi = (uint32_t)partner<LVL>((int)(uint32_t)(v >> 32));
+    return ((uint64_t)hi << 32) | lo;
+}
+
+constexpr int group_levels(int G) { return G == 16 ? 4 : (G == 32 ? 5 : 6); }
+
+// strict-'>' argmax over (need/den) with lowest feature index on ties (legacy.py:145)
+template <int LVL, int NL>
+__device__ __forceinline__ void group_argmax(int &bn, int &bd, int &bi) {
+    if constexpr (LVL < NL) {
+        const int on = partner<LVL>(bn), od = partner<LVL>(bd), oi = partner<LVL>(bi);
+        const int l = on * bd, r = bn * od;
+        const bool take = oi < kNone && (bi == kNone || l > r || (l == r && oi < bi));
+        bn = take ? on : bn;
+        bd = take ? od : bd;
+        bi = take ? oi : bi;
+        group_argmax<LVL + 1, NL>(bn, bd, bi);
+    }
+}
+
+template <int LVL, int NL>
+__device__ __forceinline__ int group_max(int v) {
+    if constexpr (LVL < NL) {
+        return group_max<LVL + 1, NL>(max(v, partner<LVL>(v)));
+    } else {
+        return v;
+    }
+}
+
+template <int LVL, int NL>
+__device__ __forceinline__ uint64_t group_sum64(uint64_t v) {
+    if constexpr (LVL < NL) {
+        return group_sum64<LVL + 1, NL>(v + partner64<LVL>(v));
+    } else {
+        return v;
+    }
+}
+
+// inclusive prefix sum inside the group (Hillis-Steele on DPP rows, row_bcast across rows)
+template <int G>
+__device__ __forceinline__ int group_scan(int v) {
+    v += dpp<0x111, 0xF, true>(0, v);
+    v += dpp<0x112, 0xF, true>(0, v);
+    v += dpp<0x114, 0xF, true>(0, v);
+    v += dpp<0x118, 0xF, true>(0, v);
+    if constexpr (G >= 32) v += dpp<0x142, 0xA>(0, v);
+    if constexpr (G == 64) v += dpp<0x143, 0xC>(0, v);
+    return v;
+}
+
+template <int G>
+__device__ __forceinline__ bool group_any(bool pred, int gbase) {
+    const uint64_t b = __ballot(pred);
+    if constexpr (G == 64) return b != 0ull;
+    else return ((b >> gbase) & ((1ull << G) - 1)) != 0ull;
+}
+
+template <int G>
+__device__ __forceinline__ uint64_t group_bits(bool pred, int gbase) {
+    const uint64_t b = __ballot(pred);
+    if constexpr (G == 64) return b;
+    else return (b >> gbase) & ((1ull << G) - 1);
+}
+
+enum : int { kContinue = -1, kAccept = 0, kFail = 1, kReject = 2, kNoCandidate = 3 };
 
 __device__ __forceinline__ void raise_status(uint32_t *status, uint32_t code, uint64_t panel) {
     if (atomicCAS(&status[0], 0u, code) == 0u) {
@@ -136,235 +219,286 @@ __device__ __forceinline__ void raise_status(uint32_t *status, uint32_t code, ui
     }
 }
 
-// One attempt of find_random_sample_legacy (legacy.py:178-200) + check_min_cats
-// (legacy.py:160-168) for one wavefront.  All branch conditions are wave-uniform.
-template <int WPL>
-__device__ int draw_attempt(const DrawArgs &A, const uint64_t *__restrict__ fm, uint64_t idx,
-                            uint64_t panel, uint32_t attempt, int lane, bool fvalid, int fmin,
-                            int fmax, int &sel, int &rem, uint64_t (&rmn)[WPL], uint64_t (&pk)[WPL]) {
-    const int W = A.W, Ws = A.Ws, k = A.k;
-    const uint32_t key0 = (uint32_t)A.seed, key1 = (uint32_t)(A.seed >> 32);
-    const uint32_t pan0 = (uint32_t)panel, pan1 = (uint32_t)(panel >> 32);
-    sel = fvalid ? A.sel0[lane] : 0;
-    rem = fvalid ? A.rem0[lane] : 0;
-#pragma unroll
-    for (int j = 0; j < WPL; ++j) {
-        const int w = lane * WPL + j;
-        rmn[j] = w < W ? A.present0[w] : 0ull;
-        pk[j] = 0ull;
-    }
-    // Philox blocks for this attempt: lane j holds block (base + j) = steps 4(base+j) .. +3
-    uint32_t blk_base = 0;
-    uint32_t x0 = (uint32_t)lane, x1 = attempt, x2 = pan0, x3 = pan1;
-    philox4x32_10(x0, x1, x2, x3, key0, key1);
-    int32_t *picks = A.picks ? A.picks + idx * (uint64_t)k : nullptr;
+// LDS layout of one workgroup: feature bitmasks F x Ws (u64) | per-group Philox words KR (u32) |
+// per-group cascade scratch W (u64)
+__host__ __device__ inline size_t draw_lds_bytes(int F, int Ws, int W, int k, int groups) {
+    const size_t KR = (size_t)((k + 3) & ~3);
+    return (size_t)F * Ws * 8 + (size_t)groups * KR * 4 + (size_t)groups * W * 8;
+}
 
-    for (int step = 0; step < k; ++step) {
-        const uint32_t blk = (uint32_t)step >> 2;
-        if (blk >= blk_base + kWave) {  // k > 256: next 64 blocks
-            blk_base += kWave;
-            x0 = blk_base + lane;
-            x1 = attempt;
-            x2 = pan0;
-            x3 = pan1;
-            philox4x32_10(x0, x1, x2, x3, key0, key1);
-        }
-        // --- find_max_ratio_cat (legacy.py:124-157) --------------------------------
-        const int need = fmin - sel;
-        if (__ballot(fvalid && sel < fmin && rem < need)) return kFail;  // legacy.py:132-137
-        const bool cand = fvalid && rem != 0 && fmax != 0 && need > -100 * rem;  // 140-141,125
-        int bn = need, bd = rem, bi = cand ? lane : kWave;
+// One LEGACY draw per G-lane group, persistent over panels i = group, group + n_groups, ...
+// Per group and step: find_max_ratio_cat (legacy.py:124-157) as a group argmax over
+// FPL features per lane, the r-th remaining holder (legacy.py:186-197) as a group prefix
+// sum over WPL bitset words per lane, delete_person + delete_all_in_cat (legacy.py:47-120)
+// in bulk bitset form, and the SelectionError / rejection tests (legacy.py:132-137,
+// 55, 73, 198-199; analysis.py:155-159).  Restarts re-key Philox with attempt + 1.
+template <int G, int FPL, int WPL>
+__global__ __launch_bounds__(kDrawThreads) void draw_kernel(DrawArgs A) {
+    constexpr int NL = group_levels(G);
+    extern __shared__ uint64_t smem[];
+    const int F = A.F, W = A.W, Ws = A.Ws, k = A.k;
+    const int KR = (k + 3) & ~3;
+    const int groups_wg = blockDim.x / G;
+    uint64_t *fm = smem;
+    uint32_t *rng_all = reinterpret_cast<uint32_t *>(smem + (size_t)F * Ws);
+    uint64_t *dscr_all = reinterpret_cast<uint64_t *>(rng_all + (size_t)groups_wg * KR);
+    for (int t = threadIdx.x; t < F * Ws; t += blockDim.x) fm[t] = A.featmask[t];
+    __syncthreads();
+
+    const int lane = threadIdx.x & 63;
+    const int glane = lane & (G - 1);
+    const int gbase = lane - glane;
+    const int gwg = threadIdx.x / G;
+    uint32_t *rng = rng_all + (size_t)gwg * KR;
+    uint64_t *dscr = dscr_all + (size_t)gwg * W;
+    const uint64_t n_groups = (uint64_t)gridDim.x * groups_wg;
+
+    int fmin[FPL], fmax[FPL], fid[FPL];
+    bool fval[FPL];
 #pragma unroll
-        for (int m = 32; m >= 1; m >>= 1) {  // argmax, strict '>' => lowest index wins ties
-            const int on = __shfl_xor(bn, m), od = __shfl_xor(bd, m), oi = __shfl_xor(bi, m);
-            const int l = on * bd, r = bn * od;
-            const bool take = oi < kWave && (bi == kWave || l > r || (l == r && oi < bi));
-            if (take) {
-                bn = on;
-                bd = od;
-                bi = oi;
+    for (int j = 0; j < FPL; ++j) {
+        fid[j] = glane * FPL + j;
+        fval[j] = fid[j] < F;
+        fmin[j] = fval[j] ? A.fmin[fid[j]] : 0;
+        fmax[j] = fval[j] ? A.fmax[fid[j]] : 0;
+    }
+    int wid[WPL];
+#pragma unroll
+    for (int j = 0; j < WPL; ++j) wid[j] = glane * WPL + j;
+
+    int sel[FPL], rem[FPL];
+    uint64_t rmn[WPL], pk[WPL];
+    uint64_t i = (uint64_t)blockIdx.x * groups_wg + gwg;
+    uint32_t a = 0;
+    int s = 0;
+    bool active = i < A.n_panels;
+    const uint32_t max_att = A.single ? 1u : A.max_attempts;
+    const uint32_t key0 = (uint32_t)A.seed, key1 = (uint32_t)(A.seed >> 32);
+
+    while (__ballot(active) != 0ull) {
+        if (!active) continue;
+        const uint64_t panel = A.panel_begin + i;
+        if (s == 0) {
+            if (a == 0 && __hip_atomic_load(&A.status[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) {
+                active = false;
+                continue;
             }
-        }
-        const int fs = __builtin_amdgcn_readfirstlane(bi);
-        bool any_present = false;
 #pragma unroll
-        for (int j = 0; j < WPL; ++j) any_present |= rmn[j] != 0ull;
-        const bool nonempty = __ballot(any_present) != 0ull;
-        int p = -1;
-        if (fs == kWave) {
-            if (nonempty) return kNoCandidate;  // KeyError at legacy.py:188
-        } else {
-            // --- randint(1, remaining) (legacy.py:149), Philox verification mode ----------
-            const uint32_t sw = (uint32_t)step & 3u;
-            const uint32_t xv = sw == 0 ? x0 : (sw == 1 ? x1 : (sw == 2 ? x2 : x3));
-            const uint32_t u = __builtin_amdgcn_readlane(xv, (int)(blk - blk_base));
-            const uint32_t remf = (uint32_t)__builtin_amdgcn_readlane(rem, fs);
-            const int r = 1 + (int)(((uint64_t)u * remf) >> 32);
-            // --- r-th remaining holder of f* in agent order (legacy.py:186-197) ------------
-            uint64_t m[WPL];
-            int cnt = 0;
+            for (int j = 0; j < FPL; ++j) {
+                sel[j] = fval[j] ? A.sel0[fid[j]] : 0;
+                rem[j] = fval[j] ? A.rem0[fid[j]] : 0;
+            }
 #pragma unroll
             for (int j = 0; j < WPL; ++j) {
-                const int w = lane * WPL + j;
-                m[j] = w < W ? (rmn[j] & fm[fs * Ws + w]) : 0ull;
-                cnt += __popcll(m[j]);
+                rmn[j] = wid[j] < W ? A.present0[wid[j]] : 0ull;
+                pk[j] = 0ull;
             }
-            int incl = cnt;
+            // Philox words of this attempt: block b covers steps 4b..4b+3 (oracle/philox.py)
+            const uint32_t att = A.attempt_base + a;
+            for (int b = glane; b < KR / 4; b += G) {
+                uint32_t x0 = (uint32_t)b, x1 = att, x2 = (uint32_t)panel, x3 = (uint32_t)(panel >> 32);
+                philox4x32_10(x0, x1, x2, x3, key0, key1);
+                rng[4 * b] = x0;
+                rng[4 * b + 1] = x1;
+                rng[4 * b + 2] = x2;
+                rng[4 * b + 3] = x3;
+            }
+        }
+        int outcome = kContinue;
+        // --- find_max_ratio_cat (legacy.py:124-157) ----------------------------------------
+        int need[FPL];
+        bool f1 = false;
 #pragma unroll
-            for (int d = 1; d < kWave; d <<= 1) {
-                const int t = __shfl_up(incl, d);
-                if (lane >= d) incl += t;
+        for (int j = 0; j < FPL; ++j) {
+            need[j] = fmin[j] - sel[j];
+            f1 |= fval[j] && sel[j] < fmin[j] && rem[j] < need[j];  // legacy.py:132-137
+        }
+        bool nonempty_lane = false;
+#pragma unroll
+        for (int j = 0; j < WPL; ++j) nonempty_lane |= rmn[j] != 0ull;
+        if (group_any<G>(f1, gbase)) {
+            outcome = kFail;
+        } else {
+            int bn = 0, bd = 1, bi = kNone;
+#pragma unroll
+            for (int j = 0; j < FPL; ++j) {
+                const bool cand = fval[j] && rem[j] != 0 && fmax[j] != 0 && need[j] > -100 * rem[j];
+                if (cand && (bi == kNone || need[j] * bd > bn * rem[j])) {
+                    bn = need[j];
+                    bd = rem[j];
+                    bi = fid[j];
+                }
             }
-            const uint64_t hit = __ballot(incl >= r);
-            if (hit) {
-                const int L = __ffsll((unsigned long long)hit) - 1;
-                int pl = 0;
-                if (lane == L) {
-                    int rr = r - (incl - cnt);
+            group_argmax<0, NL>(bn, bd, bi);
+            const bool nonempty = group_any<G>(nonempty_lane, gbase);
+            int p = -1;
+            if (bi == kNone) {
+                if (nonempty) outcome = kNoCandidate;  // KeyError at legacy.py:188
+            } else {
+                // randint(1, remaining[f*]) (legacy.py:149), Philox verification mode
+                const uint32_t u = rng[s];
+                const int r = 1 + (int)(((uint64_t)u * (uint32_t)bd) >> 32);
+                // r-th remaining holder of f* in agent order (legacy.py:186-197)
+                uint64_t m[WPL];
+                int cnt = 0;
+#pragma unroll
+                for (int j = 0; j < WPL; ++j) {
+                    m[j] = wid[j] < W ? (rmn[j] & fm[bi * Ws + wid[j]]) : 0ull;
+                    cnt += __popcll(m[j]);
+                }
+                const int incl = group_scan<G>(cnt);
+                const int excl = incl - cnt;
+                int pl = -1;
+                if (excl < r && r <= incl) {
+                    int rr = r - excl;
 #pragma unroll
                     for (int j = 0; j < WPL; ++j) {
                         const int c = __popcll(m[j]);
-                        if (rr >= 1 && rr <= c) pl = (lane * WPL + j) * 64 + select_bit(m[j], rr);
+                        if (rr >= 1 && rr <= c) pl = wid[j] * 64 + select_bit(m[j], rr);
                         rr -= c;
                     }
                 }
-                p = __builtin_amdgcn_readlane(pl, L);
-                // --- delete_person / really_delete_person (legacy.py:103-120, 67-75) -------
-                const int wi = p >> 6, bp = p & 63;
-                const uint64_t fw = fvalid ? fm[lane * Ws + wi] : 0ull;
-                const int has = (int)((fw >> bp) & 1ull);
-                sel += has;
-                rem -= has;
-                if (lane == wi / WPL) {
+                p = group_max<0, NL>(pl);
+                if (p >= 0) {
+                    // delete_person / really_delete_person (legacy.py:103-120, 67-75)
+                    const int wi = p >> 6, bp = p & 63;
+                    int has[FPL];
+                    bool anyfull = false;
 #pragma unroll
-                    for (int j = 0; j < WPL; ++j)
-                        if (j == wi % WPL) {
-                            rmn[j] &= ~(1ull << bp);
-                            pk[j] |= 1ull << bp;
+                    for (int j = 0; j < FPL; ++j) {
+                        has[j] = fval[j] ? (int)((fm[fid[j] * Ws + wi] >> bp) & 1ull) : 0;
+                        sel[j] += has[j];
+                        rem[j] -= has[j];
+                        anyfull |= has[j] && sel[j] == fmax[j];
+                    }
+                    if (glane == wi / WPL) {
+#pragma unroll
+                        for (int j = 0; j < WPL; ++j)
+                            if (j == wi % WPL) {
+                                rmn[j] &= ~(1ull << bp);
+                                pk[j] |= 1ull << bp;
+                            }
+                    }
+                    // delete_all_in_cat for each full feature of the pick (legacy.py:47-62,
+                    // 115-119), bulk form D = remaining & OR(featmask[full])
+                    if (group_any<G>(anyfull, gbase)) {
+                        uint64_t D[WPL];
+#pragma unroll
+                        for (int j = 0; j < WPL; ++j) D[j] = 0ull;
+#pragma unroll
+                        for (int jf = 0; jf < FPL; ++jf) {
+                            uint64_t bm = group_bits<G>(has[jf] && sel[jf] == fmax[jf], gbase);
+                            while (bm) {
+                                const int g = __ffsll((unsigned long long)bm) - 1;
+                                bm &= bm - 1;
+                                const int f = g * FPL + jf;
+#pragma unroll
+                                for (int j = 0; j < WPL; ++j)
+                                    if (wid[j] < W) D[j] |= fm[f * Ws + wid[j]];
+                            }
                         }
-                }
-                // --- delete_all_in_cat for every full feature of the pick (legacy.py:47-62,
-                //     115-119), bulk form: D = remaining & OR(featmask[full]) --------------
-                uint64_t full = __ballot(has && sel == fmax);
-                if (full) {
-                    uint64_t D[WPL];
-#pragma unroll
-                    for (int j = 0; j < WPL; ++j) D[j] = 0ull;
-                    while (full) {
-                        const int f = __ffsll((unsigned long long)full) - 1;
-                        full &= full - 1;
 #pragma unroll
                         for (int j = 0; j < WPL; ++j) {
-                            const int w = lane * WPL + j;
-                            if (w < W) D[j] |= fm[f * Ws + w];
+                            D[j] &= rmn[j];
+                            rmn[j] &= ~D[j];
+                            if (wid[j] < W) dscr[wid[j]] = D[j];
                         }
-                    }
-                    int dec = 0;
+                        int dec[FPL];
 #pragma unroll
-                    for (int j = 0; j < WPL; ++j) {
-                        D[j] &= rmn[j];
-                        rmn[j] &= ~D[j];
-                        uint64_t nz = __ballot(D[j] != 0ull);
-                        while (nz) {
-                            const int l = __ffsll((unsigned long long)nz) - 1;
-                            nz &= nz - 1;
-                            const int w = l * WPL + j;
-                            const uint64_t dw = readlane64(D[j], l);
-                            if (fvalid) dec += __popcll(dw & fm[lane * Ws + w]);
+                        for (int j = 0; j < FPL; ++j) dec[j] = 0;
+                        for (int w = 0; w < W; ++w) {
+                            const uint64_t dw = dscr[w];
+                            if (dw) {
+#pragma unroll
+                                for (int j = 0; j < FPL; ++j)
+                                    if (fval[j]) dec[j] += __popcll(dw & fm[fid[j] * Ws + w]);
+                            }
                         }
+#pragma unroll
+                        for (int j = 0; j < FPL; ++j) rem[j] -= dec[j];
                     }
-                    rem -= dec;
-                }
-                // remaining == 0 and selected < min raised inside the deletes (legacy.py:55,73)
-                if (__ballot(fvalid && rem == 0 && sel < fmin)) {
-                    if (picks && lane == 0) picks[step] = p;
-                    return kFail;
+                    // remaining == 0 and selected < min inside the deletes (legacy.py:55, 73)
+                    bool f2 = false;
+#pragma unroll
+                    for (int j = 0; j < FPL; ++j) f2 |= fval[j] && rem[j] == 0 && sel[j] < fmin[j];
+                    if (group_any<G>(f2, gbase)) outcome = kFail;
                 }
             }
-        }
-        if (picks && lane == 0) picks[step] = p;
-        if (step < k - 1) {  // legacy.py:198-199
-            bool any = false;
+            if (A.picks && glane == 0) A.picks[i * (uint64_t)k + s] = p;
+            if (outcome == kContinue && s < k - 1) {  // legacy.py:198-199
+                bool ne = false;
 #pragma unroll
-            for (int j = 0; j < WPL; ++j) any |= rmn[j] != 0ull;
-            if (!__ballot(any)) return kFail;
+                for (int j = 0; j < WPL; ++j) ne |= rmn[j] != 0ull;
+                if (!group_any<G>(ne, gbase)) outcome = kFail;
+            }
         }
-    }
-    if (__ballot(fvalid && sel < fmin)) return kReject;  // check_min_cats, analysis.py:155-159
-    return kAccept;
-}
-
-template <int WPL>
-__global__ __launch_bounds__(kDrawThreads) void draw_kernel(DrawArgs A) {
-    extern __shared__ uint64_t lds_fm[];
-    const int nfm = A.F * A.Ws;
-    for (int i = threadIdx.x; i < nfm; i += blockDim.x) lds_fm[i] = A.featmask[i];
-    __syncthreads();
-
-    const int lane = threadIdx.x & (kWave - 1);
-    const uint64_t wave = (uint64_t)blockIdx.x * (blockDim.x / kWave) + (threadIdx.x / kWave);
-    const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x / kWave);
-    const bool fvalid = lane < A.F;
-    const int fmin = fvalid ? A.fmin[lane] : 0;
-    const int fmax = fvalid ? A.fmax[lane] : 0;
-    const uint32_t max_att = A.single ? 1u : A.max_attempts;
-
-    for (uint64_t i = wave; i < A.n_panels; i += nwaves) {
-        if (__hip_atomic_load(&A.status[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) return;
-        const uint64_t panel = A.panel_begin + i;
-        int sel = 0, rem = 0;
-        uint64_t rmn[WPL], pk[WPL];
-        int rc = kFail;
-        uint32_t a = 0;
-        for (; a < max_att; ++a) {
-            rc = draw_attempt<WPL>(A, lds_fm, i, panel, A.attempt_base + a, lane, fvalid, fmin, fmax,
-                                   sel, rem, rmn, pk);
-            if (rc == kAccept || rc == kNoCandidate || (A.single && rc == kReject)) break;
+        if (outcome == kContinue) {
+            ++s;
+            if (s < k) continue;
+            bool under = false;  // check_min_cats (legacy.py:160-168, analysis.py:155-159)
+#pragma unroll
+            for (int j = 0; j < FPL; ++j) under |= fval[j] && sel[j] < fmin[j];
+            outcome = group_any<G>(under, gbase) ? kReject : kAccept;
         }
-        if (A.single) {  // find_random_sample_legacy: report one attempt + its final state
-            if (lane == 0) A.status[3] = (uint32_t)rc;
-            if (rc == kNoCandidate && lane == 0) raise_status(A.status, CSA_E_NO_CANDIDATE, panel);
-            if (A.sel_out && fvalid) {
-                A.sel_out[lane] = sel;
-                A.rem_out[lane] = rem;
+        // ---- attempt finished ------------------------------------------------------------
+        if (A.single) {  // find_random_sample_legacy: one attempt, report its state
+            if (glane == 0) {
+                A.status[3] = (uint32_t)outcome;
+                if (outcome == kNoCandidate) raise_status(A.status, CSA_E_NO_CANDIDATE, panel);
+            }
+            if (A.sel_out) {
+#pragma unroll
+                for (int j = 0; j < FPL; ++j)
+                    if (fval[j]) {
+                        A.sel_out[fid[j]] = sel[j];
+                        A.rem_out[fid[j]] = rem[j];
+                    }
             }
 #pragma unroll
-            for (int j = 0; j < WPL; ++j) {
-                const int w = lane * WPL + j;
-                if (w < A.W) {
-                    if (A.present_out) A.present_out[w] = rmn[j];
-                    A.panels[i * A.W + w] = pk[j];
+            for (int j = 0; j < WPL; ++j)
+                if (wid[j] < W) {
+                    if (A.present_out) A.present_out[wid[j]] = rmn[j];
+                    A.panels[i * W + wid[j]] = pk[j];
                 }
-            }
+            active = false;
             continue;
         }
-        if (rc != kAccept) {
-            if (lane == 0)
-                raise_status(A.status, rc == kNoCandidate ? CSA_E_NO_CANDIDATE : CSA_E_ATTEMPT_LIMIT, panel);
-            return;
+        if (outcome == kNoCandidate) {
+            if (glane == 0) raise_status(A.status, CSA_E_NO_CANDIDATE, panel);
+            active = false;
+            continue;
+        }
+        if (outcome != kAccept) {  // SelectionError restart or min-quota rejection
+            s = 0;
+            if (++a >= max_att) {
+                if (glane == 0) raise_status(A.status, CSA_E_ATTEMPT_LIMIT, panel);
+                active = false;
+            }
+            continue;
         }
         uint64_t h1 = 0, h2 = 0;
 #pragma unroll
         for (int j = 0; j < WPL; ++j) {
-            const uint64_t w = (uint64_t)(lane * WPL + j);
-            if (w < (uint64_t)A.W) {
-                A.panels[i * A.W + w] = pk[j];
+            const uint64_t w = (uint64_t)wid[j];
+            if (wid[j] < W) {
+                A.panels[i * W + w] = pk[j];
                 h1 += fmix_a(pk[j] ^ (w * 0x9E3779B97F4A7C15ull));
                 h2 += fmix_b(pk[j] + (w + 1) * 0xD6E8FEB86659FD93ull);
             }
         }
         if (A.hashes) {
-#pragma unroll
-            for (int m = 32; m >= 1; m >>= 1) {
-                h1 += (uint64_t)__shfl_xor((long long)h1, m);
-                h2 += (uint64_t)__shfl_xor((long long)h2, m);
-            }
-            if (lane == 0) {
+            h1 = group_sum64<0, NL>(h1);
+            h2 = group_sum64<0, NL>(h2);
+            if (glane == 0) {
                 A.hashes[2 * i] = h1;
                 A.hashes[2 * i + 1] = h2;
             }
         }
-        if (A.attempts && lane == 0) A.attempts[i] = a + 1;
+        if (A.attempts && glane == 0) A.attempts[i] = a + 1;
+        i += n_groups;
+        a = 0;
+        s = 0;
+        active = i < A.n_panels;
     }
 }
 
@@ -590,8 +724,6 @@ int dalloc(T **p, size_t count) {
     return CSA_OK;
 }
 
-int wpl_for(int W) { return W <= 64 ? 1 : (W <= 128 ? 2 : (W <= 256 ? 4 : 0)); }
-
 struct ScopedDevice {
     int prev = -1;
     explicit ScopedDevice(int dev) {
@@ -612,6 +744,62 @@ int check_k(const csa_instance *I, int32_t k) {
     return CSA_OK;
 }
 
+struct DrawConfig {
+    int G = 16, FPL = 1, WPL = 1;
+    const void *fn = nullptr;
+};
+
+template <int G, int FPL, int WPL>
+const void *draw_fn() {
+    return reinterpret_cast<const void *>(&draw_kernel<G, FPL, WPL>);
+}
+
+template <int G, int FPL>
+const void *draw_fn_w(int wpl) {
+    switch (wpl) {
+        case 1: return draw_fn<G, FPL, 1>();
+        case 2: return draw_fn<G, FPL, 2>();
+        case 4: return draw_fn<G, FPL, 4>();
+        case 8: if constexpr (G == 16) return draw_fn<G, FPL, 8>(); else return nullptr;
+        case 16: if constexpr (G == 16) return draw_fn<G, FPL, 16>(); else return nullptr;
+        default: return nullptr;
+    }
+}
+
+template <int G>
+const void *draw_fn_fw(int fpl, int wpl) {
+    switch (fpl) {
+        case 1: return draw_fn_w<G, 1>(wpl);
+        case 2: return draw_fn_w<G, 2>(wpl);
+        case 4: return draw_fn_w<G, 4>(wpl);
+        default: return nullptr;
+    }
+}
+
+int pow2_ceil_int(int x) {
+    int p = 1;
+    while (p < x) p <<= 1;
+    return p;
+}
+
+// G = 16 lanes per panel (4 panels per wavefront) unless the instance needs more lanes;
+// CSA_DRAW_GROUP=16|64 overrides (benchmarking).
+int pick_draw_config(const csa_instance *I, DrawConfig &c) {
+    int G = (I->F <= 64 && I->W <= 256) ? 16 : 64;
+    if (const char *e = getenv("CSA_DRAW_GROUP")) {
+        const int g = atoi(e);
+        if (g == 16 || g == 64) G = g;
+    }
+    c.G = G;
+    c.FPL = pow2_ceil_int((I->F + G - 1) / G);
+    c.WPL = pow2_ceil_int(std::max(1, (I->W + G - 1) / G));
+    c.fn = G == 16 ? draw_fn_fw<16>(c.FPL, c.WPL) : draw_fn_fw<64>(c.FPL, c.WPL);
+    if (!c.fn)
+        return fail(CSA_E_UNSUPPORTED, "no draw kernel for F=%d n=%d (G=%d needs FPL=%d WPL=%d)", I->F, I->n, G,
+                    c.FPL, c.WPL);
+    return CSA_OK;
+}
+
 int launch_draw(const csa_instance *I, int32_t k, uint64_t seed, uint64_t panel_begin, uint64_t n_panels,
                 uint32_t max_attempts, uint32_t attempt_base, int single, uint64_t *d_panels,
                 uint64_t *d_hashes, uint32_t *d_attempts, int32_t *d_picks, uint32_t *d_status,
@@ -620,9 +808,9 @@ int launch_draw(const csa_instance *I, int32_t k, uint64_t seed, uint64_t panel_
     if (rc) return rc;
     if (!d_panels || !d_status) return fail(CSA_E_INVALID, "d_panels and d_status are required");
     if (n_panels == 0) return CSA_OK;
-    const int wpl = wpl_for(I->W);
-    if (I->F > kWave || wpl == 0)
-        return fail(CSA_E_UNSUPPORTED, "draw kernel supports F <= 64 and n <= 16384 (F=%d n=%d)", I->F, I->n);
+    DrawConfig cfg;
+    int rc2 = pick_draw_config(I, cfg);
+    if (rc2) return rc2;
     DrawArgs A;
     A.featmask = I->d_featmask;
     A.fmin = I->d_fmin;
@@ -649,23 +837,17 @@ int launch_draw(const csa_instance *I, int32_t k, uint64_t seed, uint64_t panel_
     A.sel_out = d_sel_out;
     A.rem_out = d_rem_out;
     A.present_out = d_present_out;
-    const size_t lds = (size_t)I->F * I->Ws * sizeof(uint64_t);
-    if (lds > 160 * 1024) return fail(CSA_E_UNSUPPORTED, "feature bitmasks need %zu B of LDS", lds);
-    const void *fn = wpl == 1 ? (const void *)draw_kernel<1>
-                              : (wpl == 2 ? (const void *)draw_kernel<2> : (const void *)draw_kernel<4>);
+    const int groups_wg = kDrawThreads / cfg.G;
+    const size_t lds = draw_lds_bytes(I->F, I->Ws, I->W, k, groups_wg);
+    if (lds > 160 * 1024) return fail(CSA_E_UNSUPPORTED, "draw kernel needs %zu B of LDS", lds);
     int per_cu = 0, cus = 0;
-    HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, kDrawThreads, lds));
+    HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, cfg.fn, kDrawThreads, lds));
     HIPCHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, I->device));
-    const uint64_t waves_per_block = kDrawThreads / kWave;
-    const uint64_t want = (n_panels + waves_per_block - 1) / waves_per_block;
+    const uint64_t want = (n_panels + groups_wg - 1) / groups_wg;
     const uint64_t cap = (uint64_t)std::max(per_cu, 1) * (uint64_t)std::max(cus, 1);
     const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min(want, cap));
-    if (wpl == 1)
-        hipLaunchKernelGGL(draw_kernel<1>, dim3(grid), dim3(kDrawThreads), lds, stream, A);
-    else if (wpl == 2)
-        hipLaunchKernelGGL(draw_kernel<2>, dim3(grid), dim3(kDrawThreads), lds, stream, A);
-    else
-        hipLaunchKernelGGL(draw_kernel<4>, dim3(grid), dim3(kDrawThreads), lds, stream, A);
+    void *args[] = {&A};
+    HIPCHK(hipLaunchKernel(cfg.fn, dim3(grid), dim3(kDrawThreads), args, lds, stream));
     HIPCHK(hipGetLastError());
     return CSA_OK;
 }
