@@ -152,13 +152,14 @@ __device__ __forceinline__ uint64_t partner64(uint64_t v) {
 
 constexpr int group_levels(int G) { return G == 16 ? 4 : (G == 32 ? 5 : 6); }
 
-// strict-'>' argmax over (need/den) with lowest feature index on ties (legacy.py:145)
+// strict-'>' argmax over need/den with lowest feature index on ties (legacy.py:145); branch-free,
+// 24-bit multiplies (|need| < 2^23, den < 2^23 and need*den inside int32: checked on the host)
 template <int LVL, int NL>
 __device__ __forceinline__ void group_argmax(int &bn, int &bd, int &bi) {
     if constexpr (LVL < NL) {
         const int on = partner<LVL>(bn), od = partner<LVL>(bd), oi = partner<LVL>(bi);
-        const int l = on * bd, r = bn * od;
-        const bool take = oi < kNone && (bi == kNone || l > r || (l == r && oi < bi));
+        const int l = __mul24(on, bd), r = __mul24(bn, od);
+        const bool take = (l > r) | ((l == r) & (oi < bi));
         bn = take ? on : bn;
         bd = take ? od : bd;
         bi = take ? oi : bi;
@@ -197,17 +198,15 @@ __device__ __forceinline__ int group_scan(int v) {
 }
 
 template <int G>
-__device__ __forceinline__ bool group_any(bool pred, int gbase) {
-    const uint64_t b = __ballot(pred);
-    if constexpr (G == 64) return b != 0ull;
-    else return ((b >> gbase) & ((1ull << G) - 1)) != 0ull;
-}
-
-template <int G>
 __device__ __forceinline__ uint64_t group_bits(bool pred, int gbase) {
     const uint64_t b = __ballot(pred);
     if constexpr (G == 64) return b;
     else return (b >> gbase) & ((1ull << G) - 1);
+}
+
+template <int G>
+__device__ __forceinline__ bool group_any(bool pred, int gbase) {
+    return group_bits<G>(pred, gbase) != 0ull;
 }
 
 enum : int { kContinue = -1, kAccept = 0, kFail = 1, kReject = 2, kNoCandidate = 3 };
@@ -219,11 +218,13 @@ __device__ __forceinline__ void raise_status(uint32_t *status, uint32_t code, ui
     }
 }
 
-// LDS layout of one workgroup: feature bitmasks F x Ws (u64) | per-group Philox words KR (u32) |
-// per-group cascade scratch W (u64)
-__host__ __device__ inline size_t draw_lds_bytes(int F, int Ws, int W, int k, int groups) {
+// LDS image of the feature bitmasks: G*FPL rows (features >= F are all-zero rows with
+// min = max = remaining = 0, i.e. never candidates) of Ls = G*WPL + 1 words (odd stride:
+// lane-f reads of one word column are bank-conflict free; words >= W are zero).
+// Then per group: KR Philox words (u32) and a W-word cascade scratch row (u64).
+__host__ __device__ inline size_t draw_lds_bytes(int G, int FPL, int WPL, int W, int k, int groups) {
     const size_t KR = (size_t)((k + 3) & ~3);
-    return (size_t)F * Ws * 8 + (size_t)groups * KR * 4 + (size_t)groups * W * 8;
+    return (size_t)G * FPL * (G * WPL + 1) * 8 + (size_t)groups * KR * 4 + (size_t)groups * W * 8;
 }
 
 // One LEGACY draw per G-lane group, persistent over panels i = group, group + n_groups, ...
@@ -235,15 +236,21 @@ __host__ __device__ inline size_t draw_lds_bytes(int F, int Ws, int W, int k, in
 template <int G, int FPL, int WPL>
 __global__ __launch_bounds__(kDrawThreads) void draw_kernel(DrawArgs A) {
     constexpr int NL = group_levels(G);
+    constexpr int FR = G * FPL;        // LDS feature rows
+    constexpr int Ls = G * WPL + 1;    // LDS row stride (words)
     extern __shared__ uint64_t smem[];
-    const int F = A.F, W = A.W, Ws = A.Ws, k = A.k;
+    const int F = A.F, W = A.W, k = A.k;
     const int KR = (k + 3) & ~3;
     const int groups_wg = blockDim.x / G;
     uint64_t *fm = smem;
-    uint32_t *rng_all = reinterpret_cast<uint32_t *>(smem + (size_t)F * Ws);
+    uint32_t *rng_all = reinterpret_cast<uint32_t *>(smem + FR * Ls);
     uint64_t *dscr_all = reinterpret_cast<uint64_t *>(rng_all + (size_t)groups_wg * KR);
-    for (int t = threadIdx.x; t < F * Ws; t += blockDim.x) fm[t] = A.featmask[t];
+    for (int t = threadIdx.x; t < FR * Ls; t += blockDim.x) {
+        const int f = t / Ls, w = t - f * Ls;
+        fm[t] = (f < F && w < W) ? A.featmask[f * A.Ws + w] : 0ull;
+    }
     __syncthreads();
+    const uint32_t *fm32 = reinterpret_cast<const uint32_t *>(fm);
 
     const int lane = threadIdx.x & 63;
     const int glane = lane & (G - 1);
@@ -253,18 +260,22 @@ __global__ __launch_bounds__(kDrawThreads) void draw_kernel(DrawArgs A) {
     uint64_t *dscr = dscr_all + (size_t)gwg * W;
     const uint64_t n_groups = (uint64_t)gridDim.x * groups_wg;
 
-    int fmin[FPL], fmax[FPL], fid[FPL];
-    bool fval[FPL];
+    int fmin[FPL], fmax[FPL], fid[FPL], sel0[FPL], rem0[FPL];
 #pragma unroll
     for (int j = 0; j < FPL; ++j) {
         fid[j] = glane * FPL + j;
-        fval[j] = fid[j] < F;
-        fmin[j] = fval[j] ? A.fmin[fid[j]] : 0;
-        fmax[j] = fval[j] ? A.fmax[fid[j]] : 0;
+        const bool v = fid[j] < F;
+        fmin[j] = v ? A.fmin[fid[j]] : 0;
+        fmax[j] = v ? A.fmax[fid[j]] : 0;
+        sel0[j] = v ? A.sel0[fid[j]] : 0;
+        rem0[j] = v ? A.rem0[fid[j]] : 0;
     }
-    int wid[WPL];
+    uint64_t present0[WPL];
 #pragma unroll
-    for (int j = 0; j < WPL; ++j) wid[j] = glane * WPL + j;
+    for (int j = 0; j < WPL; ++j) {
+        const int w = glane * WPL + j;
+        present0[j] = w < W ? A.present0[w] : 0ull;
+    }
 
     int sel[FPL], rem[FPL];
     uint64_t rmn[WPL], pk[WPL];
@@ -274,231 +285,227 @@ __global__ __launch_bounds__(kDrawThreads) void draw_kernel(DrawArgs A) {
     bool active = i < A.n_panels;
     const uint32_t max_att = A.single ? 1u : A.max_attempts;
     const uint32_t key0 = (uint32_t)A.seed, key1 = (uint32_t)(A.seed >> 32);
+    if (active && __hip_atomic_load(&A.status[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) active = false;
 
     while (__ballot(active) != 0ull) {
-        if (!active) continue;
-        const uint64_t panel = A.panel_begin + i;
-        if (s == 0) {
-            if (a == 0 && __hip_atomic_load(&A.status[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) {
-                active = false;
-                continue;
-            }
+        if (active) {
+            const uint64_t panel = A.panel_begin + i;
+            if (s == 0) {  // start of an attempt (legacy_find's fresh deepcopy, analysis.py:147-148)
 #pragma unroll
-            for (int j = 0; j < FPL; ++j) {
-                sel[j] = fval[j] ? A.sel0[fid[j]] : 0;
-                rem[j] = fval[j] ? A.rem0[fid[j]] : 0;
-            }
-#pragma unroll
-            for (int j = 0; j < WPL; ++j) {
-                rmn[j] = wid[j] < W ? A.present0[wid[j]] : 0ull;
-                pk[j] = 0ull;
-            }
-            // Philox words of this attempt: block b covers steps 4b..4b+3 (oracle/philox.py)
-            const uint32_t att = A.attempt_base + a;
-            for (int b = glane; b < KR / 4; b += G) {
-                uint32_t x0 = (uint32_t)b, x1 = att, x2 = (uint32_t)panel, x3 = (uint32_t)(panel >> 32);
-                philox4x32_10(x0, x1, x2, x3, key0, key1);
-                rng[4 * b] = x0;
-                rng[4 * b + 1] = x1;
-                rng[4 * b + 2] = x2;
-                rng[4 * b + 3] = x3;
-            }
-        }
-        int outcome = kContinue;
-        // --- find_max_ratio_cat (legacy.py:124-157) ----------------------------------------
-        int need[FPL];
-        bool f1 = false;
-#pragma unroll
-        for (int j = 0; j < FPL; ++j) {
-            need[j] = fmin[j] - sel[j];
-            f1 |= fval[j] && sel[j] < fmin[j] && rem[j] < need[j];  // legacy.py:132-137
-        }
-        bool nonempty_lane = false;
-#pragma unroll
-        for (int j = 0; j < WPL; ++j) nonempty_lane |= rmn[j] != 0ull;
-        if (group_any<G>(f1, gbase)) {
-            outcome = kFail;
-        } else {
-            int bn = 0, bd = 1, bi = kNone;
-#pragma unroll
-            for (int j = 0; j < FPL; ++j) {
-                const bool cand = fval[j] && rem[j] != 0 && fmax[j] != 0 && need[j] > -100 * rem[j];
-                if (cand && (bi == kNone || need[j] * bd > bn * rem[j])) {
-                    bn = need[j];
-                    bd = rem[j];
-                    bi = fid[j];
+                for (int j = 0; j < FPL; ++j) {
+                    sel[j] = sel0[j];
+                    rem[j] = rem0[j];
                 }
-            }
-            group_argmax<0, NL>(bn, bd, bi);
-            const bool nonempty = group_any<G>(nonempty_lane, gbase);
-            int p = -1;
-            if (bi == kNone) {
-                if (nonempty) outcome = kNoCandidate;  // KeyError at legacy.py:188
-            } else {
-                // randint(1, remaining[f*]) (legacy.py:149), Philox verification mode
-                const uint32_t u = rng[s];
-                const int r = 1 + (int)(((uint64_t)u * (uint32_t)bd) >> 32);
-                // r-th remaining holder of f* in agent order (legacy.py:186-197)
-                uint64_t m[WPL];
-                int cnt = 0;
 #pragma unroll
                 for (int j = 0; j < WPL; ++j) {
-                    m[j] = wid[j] < W ? (rmn[j] & fm[bi * Ws + wid[j]]) : 0ull;
-                    cnt += __popcll(m[j]);
+                    rmn[j] = present0[j];
+                    pk[j] = 0ull;
                 }
-                const int incl = group_scan<G>(cnt);
-                const int excl = incl - cnt;
-                int pl = -1;
-                if (excl < r && r <= incl) {
-                    int rr = r - excl;
-#pragma unroll
-                    for (int j = 0; j < WPL; ++j) {
-                        const int c = __popcll(m[j]);
-                        if (rr >= 1 && rr <= c) pl = wid[j] * 64 + select_bit(m[j], rr);
-                        rr -= c;
-                    }
-                }
-                p = group_max<0, NL>(pl);
-                if (p >= 0) {
-                    // delete_person / really_delete_person (legacy.py:103-120, 67-75)
-                    const int wi = p >> 6, bp = p & 63;
-                    int has[FPL];
-                    bool anyfull = false;
-#pragma unroll
-                    for (int j = 0; j < FPL; ++j) {
-                        has[j] = fval[j] ? (int)((fm[fid[j] * Ws + wi] >> bp) & 1ull) : 0;
-                        sel[j] += has[j];
-                        rem[j] -= has[j];
-                        anyfull |= has[j] && sel[j] == fmax[j];
-                    }
-                    if (glane == wi / WPL) {
-#pragma unroll
-                        for (int j = 0; j < WPL; ++j)
-                            if (j == wi % WPL) {
-                                rmn[j] &= ~(1ull << bp);
-                                pk[j] |= 1ull << bp;
-                            }
-                    }
-                    // delete_all_in_cat for each full feature of the pick (legacy.py:47-62,
-                    // 115-119), bulk form D = remaining & OR(featmask[full])
-                    if (group_any<G>(anyfull, gbase)) {
-                        uint64_t D[WPL];
-#pragma unroll
-                        for (int j = 0; j < WPL; ++j) D[j] = 0ull;
-#pragma unroll
-                        for (int jf = 0; jf < FPL; ++jf) {
-                            uint64_t bm = group_bits<G>(has[jf] && sel[jf] == fmax[jf], gbase);
-                            while (bm) {
-                                const int g = __ffsll((unsigned long long)bm) - 1;
-                                bm &= bm - 1;
-                                const int f = g * FPL + jf;
-#pragma unroll
-                                for (int j = 0; j < WPL; ++j)
-                                    if (wid[j] < W) D[j] |= fm[f * Ws + wid[j]];
-                            }
-                        }
-#pragma unroll
-                        for (int j = 0; j < WPL; ++j) {
-                            D[j] &= rmn[j];
-                            rmn[j] &= ~D[j];
-                            if (wid[j] < W) dscr[wid[j]] = D[j];
-                        }
-                        int dec[FPL];
-#pragma unroll
-                        for (int j = 0; j < FPL; ++j) dec[j] = 0;
-                        for (int w = 0; w < W; ++w) {
-                            const uint64_t dw = dscr[w];
-                            if (dw) {
-#pragma unroll
-                                for (int j = 0; j < FPL; ++j)
-                                    if (fval[j]) dec[j] += __popcll(dw & fm[fid[j] * Ws + w]);
-                            }
-                        }
-#pragma unroll
-                        for (int j = 0; j < FPL; ++j) rem[j] -= dec[j];
-                    }
-                    // remaining == 0 and selected < min inside the deletes (legacy.py:55, 73)
-                    bool f2 = false;
-#pragma unroll
-                    for (int j = 0; j < FPL; ++j) f2 |= fval[j] && rem[j] == 0 && sel[j] < fmin[j];
-                    if (group_any<G>(f2, gbase)) outcome = kFail;
+                // Philox words of this attempt: block b covers steps 4b..4b+3 (oracle/philox.py)
+                const uint32_t att = A.attempt_base + a;
+                for (int b = glane; b < KR / 4; b += G) {
+                    uint32_t x0 = (uint32_t)b, x1 = att, x2 = (uint32_t)panel, x3 = (uint32_t)(panel >> 32);
+                    philox4x32_10(x0, x1, x2, x3, key0, key1);
+                    *reinterpret_cast<uint4 *>(rng + 4 * b) = make_uint4(x0, x1, x2, x3);
                 }
             }
-            if (A.picks && glane == 0) A.picks[i * (uint64_t)k + s] = p;
-            if (outcome == kContinue && s < k - 1) {  // legacy.py:198-199
+            int outcome = kContinue;
+            // --- find_max_ratio_cat (legacy.py:124-157) ------------------------------------
+            int need[FPL];
+            bool f1 = false;
+#pragma unroll
+            for (int j = 0; j < FPL; ++j) {
+                need[j] = fmin[j] - sel[j];
+                f1 |= (sel[j] < fmin[j]) & (rem[j] < need[j]);  // legacy.py:132-137
+            }
+            if (group_any<G>(f1, gbase)) {
+                outcome = kFail;
+            } else {
+                // sentinel ratio -100/1 = the reference's initial best (legacy.py:125): every real
+                // candidate (need > -100*rem, legacy.py:140-141) beats it, so the winner is the
+                // sentinel iff no feature is a candidate
+                int bn = -100, bd = 1, bi = fid[0];
+#pragma unroll
+                for (int j = 0; j < FPL; ++j) {
+                    const bool cand = (rem[j] != 0) & (fmax[j] != 0) & (need[j] > __mul24(-100, rem[j]));
+                    const bool take = cand & (__mul24(need[j], bd) > __mul24(bn, rem[j]));
+                    bn = take ? need[j] : bn;
+                    bd = take ? rem[j] : bd;
+                    bi = take ? fid[j] : bi;
+                }
+                group_argmax<0, NL>(bn, bd, bi);
                 bool ne = false;
 #pragma unroll
                 for (int j = 0; j < WPL; ++j) ne |= rmn[j] != 0ull;
-                if (!group_any<G>(ne, gbase)) outcome = kFail;
-            }
-        }
-        if (outcome == kContinue) {
-            ++s;
-            if (s < k) continue;
-            bool under = false;  // check_min_cats (legacy.py:160-168, analysis.py:155-159)
+                int p = -1;
+                if ((bn == -100) & (bd == 1)) {
+                    if (group_any<G>(ne, gbase)) outcome = kNoCandidate;  // KeyError, legacy.py:188
+                } else {
+                    // randint(1, remaining[f*]) (legacy.py:149), Philox verification mode
+                    const uint32_t u = rng[s];
+                    const int r = 1 + (int)__umulhi(u, (uint32_t)bd);
+                    // r-th remaining holder of f* in agent order (legacy.py:186-197)
+                    uint64_t m[WPL];
+                    int c[WPL], cnt = 0;
 #pragma unroll
-            for (int j = 0; j < FPL; ++j) under |= fval[j] && sel[j] < fmin[j];
-            outcome = group_any<G>(under, gbase) ? kReject : kAccept;
-        }
-        // ---- attempt finished ------------------------------------------------------------
-        if (A.single) {  // find_random_sample_legacy: one attempt, report its state
-            if (glane == 0) {
-                A.status[3] = (uint32_t)outcome;
-                if (outcome == kNoCandidate) raise_status(A.status, CSA_E_NO_CANDIDATE, panel);
-            }
-            if (A.sel_out) {
-#pragma unroll
-                for (int j = 0; j < FPL; ++j)
-                    if (fval[j]) {
-                        A.sel_out[fid[j]] = sel[j];
-                        A.rem_out[fid[j]] = rem[j];
+                    for (int j = 0; j < WPL; ++j) {
+                        m[j] = rmn[j] & fm[bi * Ls + glane * WPL + j];
+                        c[j] = __popcll(m[j]);
+                        cnt += c[j];
                     }
-            }
+                    const int incl = group_scan<G>(cnt);
+                    int rr = r - (incl - cnt);
+                    const bool hit = (rr >= 1) & (rr <= cnt);
+                    uint64_t ms = m[0];
+                    int js = 0;
 #pragma unroll
-            for (int j = 0; j < WPL; ++j)
-                if (wid[j] < W) {
-                    if (A.present_out) A.present_out[wid[j]] = rmn[j];
-                    A.panels[i * W + wid[j]] = pk[j];
+                    for (int j = 1; j < WPL; ++j) {
+                        const bool nxt = rr > c[j - 1];
+                        rr = nxt ? rr - c[j - 1] : rr;
+                        ms = nxt ? m[j] : ms;
+                        js = nxt ? j : js;
+                        if (!nxt) break;
+                    }
+                    const int pl = hit ? ((glane * WPL + js) * 64 + select_bit(ms, rr)) : -1;
+                    p = group_max<0, NL>(pl);
+                    if (p >= 0) {
+                        // delete_person / really_delete_person (legacy.py:103-120, 67-75)
+                        const int wi = p >> 6, bp = p & 63;
+                        bool anyfull = false;
+                        int has[FPL];
+#pragma unroll
+                        for (int j = 0; j < FPL; ++j) {
+                            has[j] = (int)((fm32[2 * (fid[j] * Ls + wi) + (bp >> 5)] >> (bp & 31)) & 1u);
+                            sel[j] += has[j];
+                            rem[j] -= has[j];
+                            anyfull |= (has[j] != 0) & (sel[j] == fmax[j]);
+                        }
+                        const uint64_t bit = 1ull << bp;
+#pragma unroll
+                        for (int j = 0; j < WPL; ++j) {
+                            const uint64_t b = (glane * WPL + j == wi) ? bit : 0ull;
+                            rmn[j] &= ~b;
+                            pk[j] |= b;
+                        }
+                        // delete_all_in_cat for every full feature of the pick (legacy.py:47-62,
+                        // 115-119), bulk form D = remaining & OR(featmask[full])
+                        if (group_any<G>(anyfull, gbase)) {
+                            uint64_t D[WPL];
+#pragma unroll
+                            for (int j = 0; j < WPL; ++j) D[j] = 0ull;
+#pragma unroll
+                            for (int jf = 0; jf < FPL; ++jf) {
+                                uint64_t bm = group_bits<G>((has[jf] != 0) & (sel[jf] == fmax[jf]), gbase);
+                                while (bm) {
+                                    const int f = (__ffsll((unsigned long long)bm) - 1) * FPL + jf;
+                                    bm &= bm - 1;
+#pragma unroll
+                                    for (int j = 0; j < WPL; ++j) D[j] |= fm[f * Ls + glane * WPL + j];
+                                }
+                            }
+#pragma unroll
+                            for (int j = 0; j < WPL; ++j) {
+                                D[j] &= rmn[j];
+                                rmn[j] &= ~D[j];
+                                if (glane * WPL + j < W) dscr[glane * WPL + j] = D[j];
+                            }
+                            int dec[FPL];
+#pragma unroll
+                            for (int j = 0; j < FPL; ++j) dec[j] = 0;
+                            for (int w = 0; w < W; ++w) {
+                                const uint64_t dw = dscr[w];
+                                if (dw) {
+#pragma unroll
+                                    for (int j = 0; j < FPL; ++j) dec[j] += __popcll(dw & fm[fid[j] * Ls + w]);
+                                }
+                            }
+#pragma unroll
+                            for (int j = 0; j < FPL; ++j) rem[j] -= dec[j];
+                        }
+                        // remaining == 0 and selected < min inside the deletes (legacy.py:55, 73)
+                        bool f2 = false;
+#pragma unroll
+                        for (int j = 0; j < FPL; ++j) f2 |= (rem[j] == 0) & (sel[j] < fmin[j]);
+                        if (group_any<G>(f2, gbase)) outcome = kFail;
+                    }
                 }
-            active = false;
-            continue;
-        }
-        if (outcome == kNoCandidate) {
-            if (glane == 0) raise_status(A.status, CSA_E_NO_CANDIDATE, panel);
-            active = false;
-            continue;
-        }
-        if (outcome != kAccept) {  // SelectionError restart or min-quota rejection
-            s = 0;
-            if (++a >= max_att) {
-                if (glane == 0) raise_status(A.status, CSA_E_ATTEMPT_LIMIT, panel);
-                active = false;
-            }
-            continue;
-        }
-        uint64_t h1 = 0, h2 = 0;
+                if (A.picks && glane == 0) A.picks[i * (uint64_t)k + s] = p;
+                if (outcome == kContinue && s < k - 1) {  // legacy.py:198-199
+                    bool ne2 = false;
 #pragma unroll
-        for (int j = 0; j < WPL; ++j) {
-            const uint64_t w = (uint64_t)wid[j];
-            if (wid[j] < W) {
-                A.panels[i * W + w] = pk[j];
-                h1 += fmix_a(pk[j] ^ (w * 0x9E3779B97F4A7C15ull));
-                h2 += fmix_b(pk[j] + (w + 1) * 0xD6E8FEB86659FD93ull);
+                    for (int j = 0; j < WPL; ++j) ne2 |= rmn[j] != 0ull;
+                    if (!group_any<G>(ne2, gbase)) outcome = kFail;
+                }
+            }
+            if (outcome == kContinue) {
+                ++s;
+                if (s == k) {  // check_min_cats (legacy.py:160-168, analysis.py:155-159)
+                    bool under = false;
+#pragma unroll
+                    for (int j = 0; j < FPL; ++j) under |= sel[j] < fmin[j];
+                    outcome = group_any<G>(under, gbase) ? kReject : kAccept;
+                }
+            }
+            if (outcome != kContinue) {
+                // ---- attempt finished -------------------------------------------------------
+                if (A.single) {  // find_random_sample_legacy: one attempt, report its state
+                    if (glane == 0) {
+                        A.status[3] = (uint32_t)outcome;
+                        if (outcome == kNoCandidate) raise_status(A.status, CSA_E_NO_CANDIDATE, panel);
+                    }
+                    if (A.sel_out) {
+#pragma unroll
+                        for (int j = 0; j < FPL; ++j)
+                            if (fid[j] < F) {
+                                A.sel_out[fid[j]] = sel[j];
+                                A.rem_out[fid[j]] = rem[j];
+                            }
+                    }
+#pragma unroll
+                    for (int j = 0; j < WPL; ++j)
+                        if (glane * WPL + j < W) {
+                            if (A.present_out) A.present_out[glane * WPL + j] = rmn[j];
+                            A.panels[i * W + glane * WPL + j] = pk[j];
+                        }
+                    active = false;
+                } else if (outcome == kNoCandidate) {
+                    if (glane == 0) raise_status(A.status, CSA_E_NO_CANDIDATE, panel);
+                    active = false;
+                } else if (outcome != kAccept) {  // SelectionError restart / min-quota rejection
+                    s = 0;
+                    if (++a >= max_att) {
+                        if (glane == 0) raise_status(A.status, CSA_E_ATTEMPT_LIMIT, panel);
+                        active = false;
+                    }
+                } else {
+                    uint64_t h1 = 0, h2 = 0;
+#pragma unroll
+                    for (int j = 0; j < WPL; ++j) {
+                        const uint64_t w = (uint64_t)(glane * WPL + j);
+                        if (w < (uint64_t)W) {
+                            A.panels[i * W + w] = pk[j];
+                            h1 += fmix_a(pk[j] ^ (w * 0x9E3779B97F4A7C15ull));
+                            h2 += fmix_b(pk[j] + (w + 1) * 0xD6E8FEB86659FD93ull);
+                        }
+                    }
+                    if (A.hashes) {
+                        h1 = group_sum64<0, NL>(h1);
+                        h2 = group_sum64<0, NL>(h2);
+                        if (glane == 0) {
+                            A.hashes[2 * i] = h1;
+                            A.hashes[2 * i + 1] = h2;
+                        }
+                    }
+                    if (A.attempts && glane == 0) A.attempts[i] = a + 1;
+                    i += n_groups;
+                    a = 0;
+                    s = 0;
+                    active = i < A.n_panels;
+                    if (active && __hip_atomic_load(&A.status[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u)
+                        active = false;
+                }
             }
         }
-        if (A.hashes) {
-            h1 = group_sum64<0, NL>(h1);
-            h2 = group_sum64<0, NL>(h2);
-            if (glane == 0) {
-                A.hashes[2 * i] = h1;
-                A.hashes[2 * i + 1] = h2;
-            }
-        }
-        if (A.attempts && glane == 0) A.attempts[i] = a + 1;
-        i += n_groups;
-        a = 0;
-        s = 0;
-        active = i < A.n_panels;
     }
 }
 
@@ -838,7 +845,7 @@ int launch_draw(const csa_instance *I, int32_t k, uint64_t seed, uint64_t panel_
     A.rem_out = d_rem_out;
     A.present_out = d_present_out;
     const int groups_wg = kDrawThreads / cfg.G;
-    const size_t lds = draw_lds_bytes(I->F, I->Ws, I->W, k, groups_wg);
+    const size_t lds = draw_lds_bytes(cfg.G, cfg.FPL, cfg.WPL, I->W, k, groups_wg);
     if (lds > 160 * 1024) return fail(CSA_E_UNSUPPORTED, "draw kernel needs %zu B of LDS", lds);
     int per_cu = 0, cus = 0;
     HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, cfg.fn, kDrawThreads, lds));
