@@ -233,7 +233,9 @@ __host__ __device__ inline size_t draw_lds_bytes(int G, int FPL, int WPL, int W,
 // sum over WPL bitset words per lane, delete_person + delete_all_in_cat (legacy.py:47-120)
 // in bulk bitset form, and the SelectionError / rejection tests (legacy.py:132-137,
 // 55, 73, 198-199; analysis.py:155-159).  Restarts re-key Philox with attempt + 1.
-template <int G, int FPL, int WPL>
+// GENERAL = false: batch mode only (panels / hashes / attempts); GENERAL = true adds pick
+// order (legacy_find) and the single-attempt state outputs (find_random_sample_legacy).
+template <int G, int FPL, int WPL, bool GENERAL>
 __global__ __launch_bounds__(kDrawThreads) void draw_kernel(DrawArgs A) {
     constexpr int NL = group_levels(G);
     constexpr int FR = G * FPL;        // LDS feature rows
@@ -283,7 +285,8 @@ __global__ __launch_bounds__(kDrawThreads) void draw_kernel(DrawArgs A) {
     uint32_t a = 0;
     int s = 0;
     bool active = i < A.n_panels;
-    const uint32_t max_att = A.single ? 1u : A.max_attempts;
+    const bool single = GENERAL && A.single;
+    const uint32_t max_att = single ? 1u : A.max_attempts;
     const uint32_t key0 = (uint32_t)A.seed, key1 = (uint32_t)(A.seed >> 32);
     if (active && __hip_atomic_load(&A.status[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) active = false;
 
@@ -358,13 +361,14 @@ __global__ __launch_bounds__(kDrawThreads) void draw_kernel(DrawArgs A) {
                     const bool hit = (rr >= 1) & (rr <= cnt);
                     uint64_t ms = m[0];
                     int js = 0;
+                    bool done = false;
 #pragma unroll
                     for (int j = 1; j < WPL; ++j) {
-                        const bool nxt = rr > c[j - 1];
+                        const bool nxt = !done & (rr > c[j - 1]);
+                        done |= !nxt;
                         rr = nxt ? rr - c[j - 1] : rr;
                         ms = nxt ? m[j] : ms;
                         js = nxt ? j : js;
-                        if (!nxt) break;
                     }
                     const int pl = hit ? ((glane * WPL + js) * 64 + select_bit(ms, rr)) : -1;
                     p = group_max<0, NL>(pl);
@@ -429,7 +433,7 @@ __global__ __launch_bounds__(kDrawThreads) void draw_kernel(DrawArgs A) {
                         if (group_any<G>(f2, gbase)) outcome = kFail;
                     }
                 }
-                if (A.picks && glane == 0) A.picks[i * (uint64_t)k + s] = p;
+                if (GENERAL && A.picks && glane == 0) A.picks[i * (uint64_t)k + s] = p;
                 if (outcome == kContinue && s < k - 1) {  // legacy.py:198-199
                     bool ne2 = false;
 #pragma unroll
@@ -448,7 +452,7 @@ __global__ __launch_bounds__(kDrawThreads) void draw_kernel(DrawArgs A) {
             }
             if (outcome != kContinue) {
                 // ---- attempt finished -------------------------------------------------------
-                if (A.single) {  // find_random_sample_legacy: one attempt, report its state
+                if (single) {  // find_random_sample_legacy: one attempt, report its state
                     if (glane == 0) {
                         A.status[3] = (uint32_t)outcome;
                         if (outcome == kNoCandidate) raise_status(A.status, CSA_E_NO_CANDIDATE, panel);
@@ -576,8 +580,10 @@ __global__ __launch_bounds__(kXtThreads) void xt_count_kernel(const uint64_t *__
 typedef int v4i __attribute__((ext_vector_type(4)));
 typedef int v16i __attribute__((ext_vector_type(16)));
 
-constexpr int kPairTile = 128;  // per wavefront: 4 x 4 MFMA tiles of 32 x 32
+constexpr int kPairBlock = 256;   // output tile per workgroup (2 x 2 waves of 128 x 128)
 constexpr int kPairThreads = 256;
+constexpr int kFragBytes = 64 * 16;                      // one 32x32 (x 32 k) int8 operand fragment
+constexpr int kPairStage = 2 * 2 * 8 * kFragBytes;       // A and B, 2 k-halves, 8 subtiles: 32 KiB
 
 // 16 bits -> 16 bytes of 0/1 (byte q*4+e = bit 4q+e)
 __device__ __forceinline__ v4i expand16(uint32_t bits) {
@@ -589,23 +595,27 @@ __device__ __forceinline__ v4i expand16(uint32_t bits) {
     return r;
 }
 
+// X^T X over panel blocks [kb0, kb1) for one 256 x 256 upper-triangular output block.
+// Per 64-panel step every thread expands one XT word of an A-row agent and one of a B-column
+// agent into four 16-byte MFMA fragments in LDS (fragment-major: [A|B][k-half][subtile][lane]),
+// double-buffered with one barrier per step; each wave then issues 2 x 4 x 4
+// v_mfma_i32_32x32x32_i8 on its 128 x 128 quadrant.  A and B fragments come from the same
+// expansion, so the k order inside a fragment cancels out of the product.
 __global__ __launch_bounds__(kPairThreads) void pair_mfma_kernel(const uint64_t *__restrict__ xt,
                                                                  uint64_t nblk, int n, int npad,
-                                                                 int ntile, int nsplit,
+                                                                 int nbt, int nsplit,
                                                                  int64_t *__restrict__ pairs) {
-    const int lane = threadIdx.x & 63;
-    const int item = __builtin_amdgcn_readfirstlane(blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6));
-    const int ntri = ntile * (ntile + 1) / 2;
-    if (item >= ntri * nsplit) return;
+    extern __shared__ __attribute__((aligned(16))) unsigned char pair_lds[];
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    const int item = blockIdx.x;
     const int tri = item / nsplit, split = item - tri * nsplit;
-    // tri -> (ti, tj) with ti <= tj, row-major over the upper triangle
-    int ti = 0, rem = tri;
-    while (rem >= ntile - ti) {
-        rem -= ntile - ti;
-        ++ti;
+    int bi = 0, rem = tri;
+    while (rem >= nbt - bi) {
+        rem -= nbt - bi;
+        ++bi;
     }
-    const int tj = ti + rem;
-    const int I0 = ti * kPairTile, J0 = tj * kPairTile;
+    const int bj = bi + rem;
+    const int I0 = bi * kPairBlock, J0 = bj * kPairBlock;
     const uint64_t per = (nblk + nsplit - 1) / nsplit;
     const uint64_t kb0 = (uint64_t)split * per, kb1 = min(nblk, kb0 + per);
 
@@ -617,34 +627,38 @@ __global__ __launch_bounds__(kPairThreads) void pair_mfma_kernel(const uint64_t 
 #pragma unroll
             for (int v = 0; v < 16; ++v) acc[a][b][v] = 0;
 
-    const int r32 = lane & 31;
-    const int hsh = 16 * (lane >> 5);
-    uint64_t wa[4], wb[4], na[4], nb[4];
+    // expansion role of this thread: agent row I0 + t (A) and column agent J0 + t (B)
+    const int sub = t >> 5, r32 = t & 31;
+    const int wr = wave >> 1, wc = wave & 1;
+    uint64_t wa = 0, wb = 0;
     if (kb0 < kb1) {
-        const uint64_t *row = xt + kb0 * (uint64_t)npad;
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-            wa[t] = row[I0 + 32 * t + r32];
-            wb[t] = row[J0 + 32 * t + r32];
-        }
+        wa = xt[kb0 * (uint64_t)npad + I0 + t];
+        wb = xt[kb0 * (uint64_t)npad + J0 + t];
     }
     for (uint64_t kb = kb0; kb < kb1; ++kb) {
-        if (kb + 1 < kb1) {  // prefetch the next panel block
-            const uint64_t *row = xt + (kb + 1) * (uint64_t)npad;
+        unsigned char *st = pair_lds + (size_t)(kb & 1) * kPairStage;
+        // expand this step's words (fragment lane = r32 + 32*h, k-half ks)
 #pragma unroll
-            for (int t = 0; t < 4; ++t) {
-                na[t] = row[I0 + 32 * t + r32];
-                nb[t] = row[J0 + 32 * t + r32];
+        for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int sh = 32 * ks + 16 * h;
+                const int off = ((ks * 8 + sub) * 64 + r32 + 32 * h) * 16;
+                *reinterpret_cast<v4i *>(st + off) = expand16((uint32_t)(wa >> sh) & 0xFFFFu);
+                *reinterpret_cast<v4i *>(st + 16 * kFragBytes + off) = expand16((uint32_t)(wb >> sh) & 0xFFFFu);
             }
+        if (kb + 1 < kb1) {  // next step's words, in flight across the barrier and the MFMAs
+            wa = xt[(kb + 1) * (uint64_t)npad + I0 + t];
+            wb = xt[(kb + 1) * (uint64_t)npad + J0 + t];
         }
+        __syncthreads();
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) {
-            const int sh = 32 * ks + hsh;
             v4i fa[4], fb[4];
 #pragma unroll
-            for (int t = 0; t < 4; ++t) {
-                fa[t] = expand16((uint32_t)(wa[t] >> sh) & 0xFFFFu);
-                fb[t] = expand16((uint32_t)(wb[t] >> sh) & 0xFFFFu);
+            for (int x = 0; x < 4; ++x) {
+                fa[x] = *reinterpret_cast<const v4i *>(st + ((ks * 8 + wr * 4 + x) * 64 + lane) * 16);
+                fb[x] = *reinterpret_cast<const v4i *>(st + 16 * kFragBytes + ((ks * 8 + wc * 4 + x) * 64 + lane) * 16);
             }
 #pragma unroll
             for (int a = 0; a < 4; ++a)
@@ -652,26 +666,25 @@ __global__ __launch_bounds__(kPairThreads) void pair_mfma_kernel(const uint64_t 
                 for (int b = 0; b < 4; ++b)
                     acc[a][b] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[a], fb[b], acc[a][b], 0, 0, 0);
         }
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-            wa[t] = na[t];
-            wb[t] = nb[t];
-        }
     }
     // C/D layout (gfx950, dtype-independent): col = lane & 31, row = (v&3) + 8*(v>>2) + 4*(lane>>5)
+    const int rbase = I0 + 128 * wr + 4 * (lane >> 5);
+    const int cbase = J0 + 128 * wc + (lane & 31);
 #pragma unroll
     for (int a = 0; a < 4; ++a)
 #pragma unroll
-        for (int b = 0; b < 4; ++b)
+        for (int b = 0; b < 4; ++b) {
+            const int col = cbase + 32 * b;
 #pragma unroll
             for (int v = 0; v < 16; ++v) {
-                const int row = I0 + 32 * a + (v & 3) + 8 * (v >> 2) + 4 * (lane >> 5);
-                const int col = J0 + 32 * b + r32;
+                const int row = rbase + 32 * a + (v & 3) + 8 * (v >> 2);
                 const int val = acc[a][b][v];
                 if (val != 0 && row < n && col < n)
                     atomicAdd(reinterpret_cast<unsigned long long *>(pairs + (uint64_t)row * n + col),
                               (unsigned long long)(long long)val);
             }
+            __builtin_amdgcn_sched_barrier(0);  // keep the 256 atomic addresses from being hoisted (VGPR spill)
+        }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -756,29 +769,29 @@ struct DrawConfig {
     const void *fn = nullptr;
 };
 
-template <int G, int FPL, int WPL>
+template <int G, int FPL, int WPL, bool GEN>
 const void *draw_fn() {
-    return reinterpret_cast<const void *>(&draw_kernel<G, FPL, WPL>);
+    return reinterpret_cast<const void *>(&draw_kernel<G, FPL, WPL, GEN>);
 }
 
-template <int G, int FPL>
+template <int G, int FPL, bool GEN>
 const void *draw_fn_w(int wpl) {
     switch (wpl) {
-        case 1: return draw_fn<G, FPL, 1>();
-        case 2: return draw_fn<G, FPL, 2>();
-        case 4: return draw_fn<G, FPL, 4>();
-        case 8: if constexpr (G == 16) return draw_fn<G, FPL, 8>(); else return nullptr;
-        case 16: if constexpr (G == 16) return draw_fn<G, FPL, 16>(); else return nullptr;
+        case 1: return draw_fn<G, FPL, 1, GEN>();
+        case 2: return draw_fn<G, FPL, 2, GEN>();
+        case 4: return draw_fn<G, FPL, 4, GEN>();
+        case 8: if constexpr (G == 16) return draw_fn<G, FPL, 8, GEN>(); else return nullptr;
+        case 16: if constexpr (G == 16) return draw_fn<G, FPL, 16, GEN>(); else return nullptr;
         default: return nullptr;
     }
 }
 
-template <int G>
+template <int G, bool GEN>
 const void *draw_fn_fw(int fpl, int wpl) {
     switch (fpl) {
-        case 1: return draw_fn_w<G, 1>(wpl);
-        case 2: return draw_fn_w<G, 2>(wpl);
-        case 4: return draw_fn_w<G, 4>(wpl);
+        case 1: return draw_fn_w<G, 1, GEN>(wpl);
+        case 2: return draw_fn_w<G, 2, GEN>(wpl);
+        case 4: return draw_fn_w<G, 4, GEN>(wpl);
         default: return nullptr;
     }
 }
@@ -789,18 +802,22 @@ int pow2_ceil_int(int x) {
     return p;
 }
 
-// G = 16 lanes per panel (4 panels per wavefront) unless the instance needs more lanes;
-// CSA_DRAW_GROUP=16|64 overrides (benchmarking).
-int pick_draw_config(const csa_instance *I, DrawConfig &c) {
-    int G = (I->F <= 64 && I->W <= 256) ? 16 : 64;
+// Batch draws: G = 16 lanes per panel (4 panels per wavefront) unless the instance needs more
+// lanes; CSA_DRAW_GROUP=16|64 overrides (benchmarking).  Pick-order / single-attempt draws
+// (general mode) use the G = 64 kernels.
+int pick_draw_config(const csa_instance *I, bool general, DrawConfig &c) {
+    int G = (!general && I->F <= 64 && I->W <= 256) ? 16 : 64;
     if (const char *e = getenv("CSA_DRAW_GROUP")) {
         const int g = atoi(e);
-        if (g == 16 || g == 64) G = g;
+        if (!general && (g == 16 || g == 64)) G = g;
     }
     c.G = G;
     c.FPL = pow2_ceil_int((I->F + G - 1) / G);
     c.WPL = pow2_ceil_int(std::max(1, (I->W + G - 1) / G));
-    c.fn = G == 16 ? draw_fn_fw<16>(c.FPL, c.WPL) : draw_fn_fw<64>(c.FPL, c.WPL);
+    if (general)
+        c.fn = draw_fn_fw<64, true>(c.FPL, c.WPL);
+    else
+        c.fn = G == 16 ? draw_fn_fw<16, false>(c.FPL, c.WPL) : draw_fn_fw<64, false>(c.FPL, c.WPL);
     if (!c.fn)
         return fail(CSA_E_UNSUPPORTED, "no draw kernel for F=%d n=%d (G=%d needs FPL=%d WPL=%d)", I->F, I->n, G,
                     c.FPL, c.WPL);
@@ -816,7 +833,7 @@ int launch_draw(const csa_instance *I, int32_t k, uint64_t seed, uint64_t panel_
     if (!d_panels || !d_status) return fail(CSA_E_INVALID, "d_panels and d_status are required");
     if (n_panels == 0) return CSA_OK;
     DrawConfig cfg;
-    int rc2 = pick_draw_config(I, cfg);
+    int rc2 = pick_draw_config(I, single || d_picks || d_sel_out || d_present_out, cfg);
     if (rc2) return rc2;
     DrawArgs A;
     A.featmask = I->d_featmask;
@@ -1035,7 +1052,7 @@ int csa_draw_async(const csa_instance *I, int32_t k, uint64_t seed, uint64_t pan
                        d_picks, d_status, nullptr, nullptr, nullptr, (hipStream_t)stream);
 }
 
-int32_t csa_xt_pad(int32_t n) { return ((n + kPairTile - 1) / kPairTile) * kPairTile; }
+int32_t csa_xt_pad(int32_t n) { return ((n + kPairBlock - 1) / kPairBlock) * kPairBlock; }
 
 int csa_transpose_count_async(const uint64_t *d_panels, uint64_t n_panels, int32_t n, uint64_t *d_xt,
                               int64_t *d_counts, void *stream) {
@@ -1056,14 +1073,20 @@ int csa_pair_counts_async(const uint64_t *d_xt, uint64_t n_blocks, int32_t n, in
     if (n <= 0 || !d_xt || !d_pairs) return fail(CSA_E_INVALID, "pairs: bad arguments");
     if (n_blocks == 0) return CSA_OK;
     if (n_blocks * 64 >= (1ull << 31)) return fail(CSA_E_UNSUPPORTED, "pairs: > 2^31 panels per call");
-    const int npad = csa_xt_pad(n), ntile = npad / kPairTile;
-    const int ntri = ntile * (ntile + 1) / 2;
-    // enough (tile, split) work items to fill 256 CUs x 4 SIMDs twice, >= 8 panel blocks each
-    int nsplit = std::max(1, (2048 + ntri - 1) / ntri);
+    const int npad = csa_xt_pad(n), nbt = npad / kPairBlock;
+    const int ntri = nbt * (nbt + 1) / 2;
+    // one 256-thread workgroup per CU (256 accumulator AGPRs per wave): fill the 256 CUs once,
+    // keeping >= 8 panel blocks per split
+    int cus = 256;
+    {
+        int dev = 0;
+        if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    }
+    int nsplit = std::max(1, cus / ntri);
     nsplit = (int)std::min<uint64_t>((uint64_t)nsplit, std::max<uint64_t>(1, n_blocks / 8));
-    const int waves = ntri * nsplit, wpb = kPairThreads / 64;
-    hipLaunchKernelGGL(pair_mfma_kernel, dim3((waves + wpb - 1) / wpb), dim3(kPairThreads), 0,
-                       (hipStream_t)stream, d_xt, n_blocks, n, npad, ntile, nsplit, d_pairs);
+    const size_t lds = 2 * (size_t)kPairStage;
+    hipLaunchKernelGGL(pair_mfma_kernel, dim3(ntri * nsplit), dim3(kPairThreads), lds, (hipStream_t)stream, d_xt,
+                       n_blocks, n, npad, nbt, nsplit, d_pairs);
     HIPCHK(hipGetLastError());
     return CSA_OK;
 }

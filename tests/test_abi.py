@@ -33,7 +33,7 @@ def test_version_and_error_plumbing():
     rc = L.csa_instance_create(-1, 0, 0, None, None, None, None, ctypes.byref(h))
     assert rc == N.CSA_E_INVALID
     assert "invalid" in N.last_error()
-    assert L.csa_xt_pad(1) == 128 and L.csa_xt_pad(1727) == 1792
+    assert L.csa_xt_pad(1) == 256 and L.csa_xt_pad(1727) == 1792 and L.csa_xt_pad(2000) == 2048
 
 
 def test_no_cpu_fallback_when_library_missing(monkeypatch, tmp_path):

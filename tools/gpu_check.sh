@@ -41,4 +41,13 @@ rc=$?
 echo "[rocprofv3] rc=$rc"
 tail -3 "$OUT/prof_$TAG.err"
 find "$OUT/prof_$TAG" -name "*stats*" | head
+[ $rc -eq 0 ] || exit $rc
+if [ "${PMC:-0}" = "1" ]; then
+    echo "== rocprofv3 pmc (SQ instruction mix)"
+    timeout -k 10 400 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU \
+        --output-format csv -d "$OUT/prof_$TAG/pmc_sq1" -o run -- \
+        python3 "$ROOT/bench.py" --steps 2 --warmup 1 --no-cpu-baseline > /dev/null 2> "$OUT/prof_${TAG}_pmc.err"
+    rc=$?
+    echo "[pmc] rc=$rc"
+fi
 exit $rc
