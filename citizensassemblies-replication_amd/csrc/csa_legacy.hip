@@ -630,14 +630,9 @@ __global__ __launch_bounds__(kPairThreads) void pair_mfma_kernel(const uint64_t 
     // expansion role of this thread: agent row I0 + t (A) and column agent J0 + t (B)
     const int sub = t >> 5, r32 = t & 31;
     const int wr = wave >> 1, wc = wave & 1;
-    uint64_t wa = 0, wb = 0;
-    if (kb0 < kb1) {
-        wa = xt[kb0 * (uint64_t)npad + I0 + t];
-        wb = xt[kb0 * (uint64_t)npad + J0 + t];
-    }
-    for (uint64_t kb = kb0; kb < kb1; ++kb) {
-        unsigned char *st = pair_lds + (size_t)(kb & 1) * kPairStage;
-        // expand this step's words (fragment lane = r32 + 32*h, k-half ks)
+    // software pipeline: step kb's fragments are read from LDS stage kb&1 while step kb+1's
+    // words are expanded into the other stage and step kb+2's words are loaded
+    auto expand_to = [&](unsigned char *st, uint64_t wa, uint64_t wb) {
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
@@ -647,25 +642,57 @@ __global__ __launch_bounds__(kPairThreads) void pair_mfma_kernel(const uint64_t 
                 *reinterpret_cast<v4i *>(st + off) = expand16((uint32_t)(wa >> sh) & 0xFFFFu);
                 *reinterpret_cast<v4i *>(st + 16 * kFragBytes + off) = expand16((uint32_t)(wb >> sh) & 0xFFFFu);
             }
-        if (kb + 1 < kb1) {  // next step's words, in flight across the barrier and the MFMAs
-            wa = xt[(kb + 1) * (uint64_t)npad + I0 + t];
-            wb = xt[(kb + 1) * (uint64_t)npad + J0 + t];
+    };
+    uint64_t na = 0, nb = 0;
+    if (kb0 < kb1) {
+        expand_to(pair_lds + (size_t)(kb0 & 1) * kPairStage, xt[kb0 * (uint64_t)npad + I0 + t],
+                  xt[kb0 * (uint64_t)npad + J0 + t]);
+        if (kb0 + 1 < kb1) {
+            na = xt[(kb0 + 1) * (uint64_t)npad + I0 + t];
+            nb = xt[(kb0 + 1) * (uint64_t)npad + J0 + t];
         }
-        __syncthreads();
+    }
+    __syncthreads();
+    for (uint64_t kb = kb0; kb < kb1; ++kb) {
+        const unsigned char *st = pair_lds + (size_t)(kb & 1) * kPairStage;
+        v4i fa[2][4], fb[2][4];
 #pragma unroll
-        for (int ks = 0; ks < 2; ++ks) {
-            v4i fa[4], fb[4];
+        for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
             for (int x = 0; x < 4; ++x) {
-                fa[x] = *reinterpret_cast<const v4i *>(st + ((ks * 8 + wr * 4 + x) * 64 + lane) * 16);
-                fb[x] = *reinterpret_cast<const v4i *>(st + 16 * kFragBytes + ((ks * 8 + wc * 4 + x) * 64 + lane) * 16);
+                fa[ks][x] = *reinterpret_cast<const v4i *>(st + ((ks * 8 + wr * 4 + x) * 64 + lane) * 16);
+                fb[ks][x] = *reinterpret_cast<const v4i *>(st + 16 * kFragBytes + ((ks * 8 + wc * 4 + x) * 64 + lane) * 16);
             }
+        // unconditional (the last step expands into the unused stage) so that one basic block
+        // holds reads, expansion and MFMAs and the scheduler can interleave them
+        expand_to(pair_lds + (size_t)((kb + 1) & 1) * kPairStage, na, nb);
+        {
+            const uint64_t nk = min(kb + 2, kb1 - 1);
+            na = xt[nk * (uint64_t)npad + I0 + t];
+            nb = xt[nk * (uint64_t)npad + J0 + t];
+        }
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
             for (int a = 0; a < 4; ++a)
 #pragma unroll
                 for (int b = 0; b < 4; ++b)
-                    acc[a][b] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[a], fb[b], acc[a][b], 0, 0, 0);
+                    acc[a][b] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[ks][a], fb[ks][b], acc[a][b], 0, 0, 0);
+        // interleave: 16 LDS reads, then per MFMA ~3 VALU of the next step's expansion and one
+        // LDS write every 4 MFMAs
+        __builtin_amdgcn_sched_group_barrier(0x100, 16, 0);
+#pragma unroll
+        for (int g = 0; g < 8; ++g) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);
+            __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
         }
+        __syncthreads();
     }
     // C/D layout (gfx950, dtype-independent): col = lane & 31, row = (v&3) + 8*(v>>2) + 4*(lane>>5)
     const int rbase = I0 + 128 * wr + 4 * (lane >> 5);
