@@ -580,32 +580,31 @@ __global__ __launch_bounds__(kXtThreads) void xt_count_kernel(const uint64_t *__
 typedef int v4i __attribute__((ext_vector_type(4)));
 typedef int v16i __attribute__((ext_vector_type(16)));
 
-constexpr int kPairBlock = 256;   // output tile per workgroup (2 x 2 waves of 128 x 128)
-constexpr int kPairThreads = 256;
-constexpr int kFragBytes = 64 * 16;                      // one 32x32 (x 32 k) int8 operand fragment
-constexpr int kPairStage = 2 * 2 * 8 * kFragBytes;       // A and B, 2 k-halves, 8 subtiles: 32 KiB
+constexpr int kPairBlock = 256;   // output tile per workgroup: 8 waves of 128 rows x 64 columns
+constexpr int kPairThreads = 512;
 
-// 16 bits -> 16 bytes of 0/1 (byte q*4+e = bit 4q+e)
-__device__ __forceinline__ v4i expand16(uint32_t bits) {
+// MFMA operand fragment (k-half ks, lane half h) of one XT word w: dword q holds the four bits
+// 4h+q, 4h+q+8, 4h+q+16, 4h+q+24 of the 32-bit half ks as int8 0/1 values (2 VALU per dword).
+// Any fixed bit->k placement works because A and B fragments use the same one (the k order
+// cancels in the sum over k), and the four (ks, h) fragments cover all 64 panels once.
+__device__ __forceinline__ v4i xt_frag(uint64_t w, int ks, int h) {
+    const uint32_t x = (uint32_t)(w >> (32 * ks));
     v4i r;
-    r[0] = (int)(((bits & 0xFu) * 0x00204081u) & 0x01010101u);
-    r[1] = (int)((((bits >> 4) & 0xFu) * 0x00204081u) & 0x01010101u);
-    r[2] = (int)((((bits >> 8) & 0xFu) * 0x00204081u) & 0x01010101u);
-    r[3] = (int)((((bits >> 12) & 0xFu) * 0x00204081u) & 0x01010101u);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) r[q] = (int)((x >> (4 * h + q)) & 0x01010101u);
     return r;
 }
 
 // X^T X over panel blocks [kb0, kb1) for one 256 x 256 upper-triangular output block.
-// Per 64-panel step every thread expands one XT word of an A-row agent and one of a B-column
-// agent into four 16-byte MFMA fragments in LDS (fragment-major: [A|B][k-half][subtile][lane]),
-// double-buffered with one barrier per step; each wave then issues 2 x 4 x 4
-// v_mfma_i32_32x32x32_i8 on its 128 x 128 quadrant.  A and B fragments come from the same
-// expansion, so the k order inside a fragment cancels out of the product.
+// Per 64-panel step the 512 threads stage the packed XT words of the block's 256 rows and 256
+// columns in LDS (4 KiB, double-buffered, one barrier per step); wave (wr, wc) reads the words
+// of its 128 rows and 64 columns, expands them into int8 fragments in registers and issues
+// 2 x 4 x 2 v_mfma_i32_32x32x32_i8 (two waves per SIMD interleave expansion and MFMA).
 __global__ __launch_bounds__(kPairThreads) void pair_mfma_kernel(const uint64_t *__restrict__ xt,
                                                                  uint64_t nblk, int n, int npad,
                                                                  int nbt, int nsplit,
                                                                  int64_t *__restrict__ pairs) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char pair_lds[];
+    __shared__ uint64_t words[2][2 * kPairBlock];
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
     const int item = blockIdx.x;
     const int tri = item / nsplit, split = item - tri * nsplit;
@@ -619,88 +618,54 @@ __global__ __launch_bounds__(kPairThreads) void pair_mfma_kernel(const uint64_t 
     const uint64_t per = (nblk + nsplit - 1) / nsplit;
     const uint64_t kb0 = (uint64_t)split * per, kb1 = min(nblk, kb0 + per);
 
-    v16i acc[4][4];
+    v16i acc[4][2];
 #pragma unroll
     for (int a = 0; a < 4; ++a)
 #pragma unroll
-        for (int b = 0; b < 4; ++b)
+        for (int b = 0; b < 2; ++b)
 #pragma unroll
             for (int v = 0; v < 16; ++v) acc[a][b][v] = 0;
 
-    // expansion role of this thread: agent row I0 + t (A) and column agent J0 + t (B)
-    const int sub = t >> 5, r32 = t & 31;
-    const int wr = wave >> 1, wc = wave & 1;
-    // software pipeline: step kb's fragments are read from LDS stage kb&1 while step kb+1's
-    // words are expanded into the other stage and step kb+2's words are loaded
-    auto expand_to = [&](unsigned char *st, uint64_t wa, uint64_t wb) {
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                const int sh = 32 * ks + 16 * h;
-                const int off = ((ks * 8 + sub) * 64 + r32 + 32 * h) * 16;
-                *reinterpret_cast<v4i *>(st + off) = expand16((uint32_t)(wa >> sh) & 0xFFFFu);
-                *reinterpret_cast<v4i *>(st + 16 * kFragBytes + off) = expand16((uint32_t)(wb >> sh) & 0xFFFFu);
-            }
-    };
-    uint64_t na = 0, nb = 0;
+    const int wr = wave >> 2, wc = wave & 3;
+    const int r32 = lane & 31, h = lane >> 5;
+    const int src = t < kPairBlock ? I0 + t : J0 + t - kPairBlock;  // staging role of this thread
+    uint64_t nw = 0;
     if (kb0 < kb1) {
-        expand_to(pair_lds + (size_t)(kb0 & 1) * kPairStage, xt[kb0 * (uint64_t)npad + I0 + t],
-                  xt[kb0 * (uint64_t)npad + J0 + t]);
-        if (kb0 + 1 < kb1) {
-            na = xt[(kb0 + 1) * (uint64_t)npad + I0 + t];
-            nb = xt[(kb0 + 1) * (uint64_t)npad + J0 + t];
-        }
+        words[kb0 & 1][t] = xt[kb0 * (uint64_t)npad + src];
+        nw = xt[min(kb0 + 1, kb1 - 1) * (uint64_t)npad + src];
     }
     __syncthreads();
     for (uint64_t kb = kb0; kb < kb1; ++kb) {
-        const unsigned char *st = pair_lds + (size_t)(kb & 1) * kPairStage;
-        v4i fa[2][4], fb[2][4];
+        const uint64_t *w = words[kb & 1];
+        uint64_t wa[4], wb[2];
 #pragma unroll
-        for (int ks = 0; ks < 2; ++ks)
+        for (int x = 0; x < 4; ++x) wa[x] = w[128 * wr + 32 * x + r32];
 #pragma unroll
-            for (int x = 0; x < 4; ++x) {
-                fa[ks][x] = *reinterpret_cast<const v4i *>(st + ((ks * 8 + wr * 4 + x) * 64 + lane) * 16);
-                fb[ks][x] = *reinterpret_cast<const v4i *>(st + 16 * kFragBytes + ((ks * 8 + wc * 4 + x) * 64 + lane) * 16);
-            }
-        // unconditional (the last step expands into the unused stage) so that one basic block
-        // holds reads, expansion and MFMAs and the scheduler can interleave them
-        expand_to(pair_lds + (size_t)((kb + 1) & 1) * kPairStage, na, nb);
-        {
-            const uint64_t nk = min(kb + 2, kb1 - 1);
-            na = xt[nk * (uint64_t)npad + I0 + t];
-            nb = xt[nk * (uint64_t)npad + J0 + t];
-        }
+        for (int x = 0; x < 2; ++x) wb[x] = w[kPairBlock + 64 * wc + 32 * x + r32];
+        words[(kb + 1) & 1][t] = nw;  // the last step stages a duplicate nobody reads
+        nw = xt[min(kb + 2, kb1 - 1) * (uint64_t)npad + src];
 #pragma unroll
-        for (int ks = 0; ks < 2; ++ks)
+        for (int ks = 0; ks < 2; ++ks) {
+            v4i fa[4], fb[2];
+#pragma unroll
+            for (int x = 0; x < 4; ++x) fa[x] = xt_frag(wa[x], ks, h);
+#pragma unroll
+            for (int x = 0; x < 2; ++x) fb[x] = xt_frag(wb[x], ks, h);
 #pragma unroll
             for (int a = 0; a < 4; ++a)
 #pragma unroll
-                for (int b = 0; b < 4; ++b)
-                    acc[a][b] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[ks][a], fb[ks][b], acc[a][b], 0, 0, 0);
-        // interleave: 16 LDS reads, then per MFMA ~3 VALU of the next step's expansion and one
-        // LDS write every 4 MFMAs
-        __builtin_amdgcn_sched_group_barrier(0x100, 16, 0);
-#pragma unroll
-        for (int g = 0; g < 8; ++g) {
-            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-            __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);
-            __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);
-            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-            __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);
-            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-            __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);
-            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                for (int b = 0; b < 2; ++b)
+                    acc[a][b] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[a], fb[b], acc[a][b], 0, 0, 0);
         }
         __syncthreads();
     }
     // C/D layout (gfx950, dtype-independent): col = lane & 31, row = (v&3) + 8*(v>>2) + 4*(lane>>5)
-    const int rbase = I0 + 128 * wr + 4 * (lane >> 5);
-    const int cbase = J0 + 128 * wc + (lane & 31);
+    const int rbase = I0 + 128 * wr + 4 * h;
+    const int cbase = J0 + 64 * wc + r32;
 #pragma unroll
     for (int a = 0; a < 4; ++a)
 #pragma unroll
-        for (int b = 0; b < 4; ++b) {
+        for (int b = 0; b < 2; ++b) {
             const int col = cbase + 32 * b;
 #pragma unroll
             for (int v = 0; v < 16; ++v) {
@@ -710,7 +675,7 @@ __global__ __launch_bounds__(kPairThreads) void pair_mfma_kernel(const uint64_t 
                     atomicAdd(reinterpret_cast<unsigned long long *>(pairs + (uint64_t)row * n + col),
                               (unsigned long long)(long long)val);
             }
-            __builtin_amdgcn_sched_barrier(0);  // keep the 256 atomic addresses from being hoisted (VGPR spill)
+            __builtin_amdgcn_sched_barrier(0);  // keep the atomic addresses from being hoisted (VGPR spill)
         }
 }
 
@@ -1102,7 +1067,7 @@ int csa_pair_counts_async(const uint64_t *d_xt, uint64_t n_blocks, int32_t n, in
     if (n_blocks * 64 >= (1ull << 31)) return fail(CSA_E_UNSUPPORTED, "pairs: > 2^31 panels per call");
     const int npad = csa_xt_pad(n), nbt = npad / kPairBlock;
     const int ntri = nbt * (nbt + 1) / 2;
-    // one 256-thread workgroup per CU (256 accumulator AGPRs per wave): fill the 256 CUs once,
+    // one 512-thread workgroup per CU (128 accumulator registers per wave): fill the 256 CUs once,
     // keeping >= 8 panel blocks per split
     int cus = 256;
     {
@@ -1111,8 +1076,7 @@ int csa_pair_counts_async(const uint64_t *d_xt, uint64_t n_blocks, int32_t n, in
     }
     int nsplit = std::max(1, cus / ntri);
     nsplit = (int)std::min<uint64_t>((uint64_t)nsplit, std::max<uint64_t>(1, n_blocks / 8));
-    const size_t lds = 2 * (size_t)kPairStage;
-    hipLaunchKernelGGL(pair_mfma_kernel, dim3(ntri * nsplit), dim3(kPairThreads), lds, (hipStream_t)stream, d_xt,
+    hipLaunchKernelGGL(pair_mfma_kernel, dim3(ntri * nsplit), dim3(kPairThreads), 0, (hipStream_t)stream, d_xt,
                        n_blocks, n, npad, nbt, nsplit, d_pairs);
     HIPCHK(hipGetLastError());
     return CSA_OK;

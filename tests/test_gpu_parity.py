@@ -212,3 +212,38 @@ def test_device_pipeline_matches_host_api(gpu_available):
     iu = np.triu_indices(enc.n, 1)
     assert np.array_equal(pipe.pairs.cpu().numpy().reshape(enc.n, enc.n)[iu], raw.pairs[iu])
     torch.cuda.synchronize()
+
+
+def test_unique_hashes_owner_partition(gpu_available):
+    """csa_unique_hashes_async (multi-GPU distinct-panel step): per-owner counts sum to the total."""
+    import torch
+    D = pkg("distributed")
+    N = pkg("_native")
+    o = oracle_read(*inst_paths("example_small_20"), 20)
+    rc, panels, _, _ = coracle.draw(o, 20, 3, 0, 5000)
+    panels = np.concatenate([panels, panels[:700]])           # 700 duplicates
+    h = torch.from_numpy(D.panel_hashes(panels).ravel().view(np.int64).copy()).cuda()
+    table = D.HashTable(h.numel() // 2, h.device)
+    total = 0
+    for world in (1, 2, 3, 8):
+        total = 0
+        for r in range(world):
+            table.count.zero_()
+            N.check(N.lib().csa_unique_hashes_async(N.ptr(h), h.numel() // 2, world, r, N.ptr(table.table),
+                                                    table.slots, N.ptr(table.count), None))
+            torch.cuda.synchronize()
+            total += int(table.count.item())
+        assert total == coracle.unique(panels, o.n) == 5000
+
+
+def test_device_hashes_match_host_mirror(gpu_available):
+    """The draw kernel's 128-bit panel hash == distributed.panel_hashes (used by the gloo path)."""
+    D = pkg("distributed")
+    Dv = pkg("device")
+    inst, enc = _enc("sf_e_110", 110)
+    pipe = Dv.DevicePipeline(enc, 110, 4096, want_pairs=False)
+    pipe.reset()
+    pipe.run(1, 77, 4096)
+    pipe.check_status()
+    dev_h = pipe.hashes.cpu().numpy().view(np.uint64).reshape(-1, 2)
+    assert np.array_equal(dev_h, D.panel_hashes(pipe.panels_view(4096)))
