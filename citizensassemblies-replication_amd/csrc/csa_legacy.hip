@@ -235,8 +235,11 @@ __host__ __device__ inline size_t draw_lds_bytes(int G, int FPL, int WPL, int W,
 // 55, 73, 198-199; analysis.py:155-159).  Restarts re-key Philox with attempt + 1.
 // GENERAL = false: batch mode only (panels / hashes / attempts); GENERAL = true adds pick
 // order (legacy_find) and the single-attempt state outputs (find_random_sample_legacy).
+// waves per SIMD requested from the register allocator: small instances fit 6 (80 VGPRs)
+constexpr int draw_occupancy(int FPL, int WPL) { return FPL + WPL <= 4 ? 6 : 1; }
+
 template <int G, int FPL, int WPL, bool GENERAL>
-__global__ __launch_bounds__(kDrawThreads) void draw_kernel(DrawArgs A) {
+__global__ __launch_bounds__(kDrawThreads, draw_occupancy(FPL, WPL)) void draw_kernel(DrawArgs A) {
     constexpr int NL = group_levels(G);
     constexpr int FR = G * FPL;        // LDS feature rows
     constexpr int Ls = G * WPL + 1;    // LDS row stride (words)
