@@ -225,6 +225,8 @@ def main():
         traffic = None
         if pmc and pmc.get("kernel") == name and pmc.get("panels") == S:
             traffic = pmc.get("hbm_bytes_per_launch")
+        if pmc and name == "draw_kernel" and pmc.get("draw_issue"):
+            kernels["draw"]["pmc_issue"] = pmc["draw_issue"]     # committed rocprofv3 --pmc pass
         roof = {"kernel": name, "bound": "hbm", "achieved": ach, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
                 "frac": ach * 1e9 / HBM_PEAK, "traffic": traffic,
                 "note": "draw_kernel is VALU/LDS issue-bound; its HBM bytes are the panel+hash writes"}
