@@ -30,6 +30,9 @@ PKG = "citizensassemblies-replication_amd"
 
 HBM_PEAK = 8.0e12          # B/s, MI355X spec (MI355X_MICROARCH.md)
 I8_MFMA_PEAK = 5.03e15     # dense int8 ops/s: 2x the 2.5 PF bf16 dense rate (MI355X_MICROARCH.md)
+FP4_MFMA_PEAK = 10.06e15   # dense fp4 ops/s (scaled f8f6f4 MFMA): 4x the bf16 dense rate (MI355X_MICROARCH.md)
+PAIR_ENGINES = {"fp4": (0, FP4_MFMA_PEAK, "fp4 e2m1 operands (exact 0/1 products), f32 accumulation"),
+                "i8": (1, I8_MFMA_PEAK, "int8 operands, int32 accumulation")}
 
 CONFIGS = {
     # name: (instance dir, k, default panels per GPU per step)
@@ -50,6 +53,7 @@ def parse():
     ap.add_argument("--panels", type=int, default=0, help="panels per GPU per step (0 = config default)")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--no-pairs", action="store_true")
+    ap.add_argument("--pair-engine", default="fp4", choices=sorted(PAIR_ENGINES))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample duration")
     return ap.parse_args()
@@ -131,7 +135,9 @@ def main():
     enc.check_quotas(k)
     want_pairs = not args.no_pairs
     stream = torch.cuda.current_stream(dev)
-    pipe = Dv.DevicePipeline(enc, k, S, want_pairs=want_pairs, want_unique=True, device=dev, stream=stream)
+    engine_id, engine_peak, engine_desc = PAIR_ENGINES[args.pair_engine]
+    pipe = Dv.DevicePipeline(enc, k, S, want_pairs=want_pairs, want_unique=True, device=dev, stream=stream,
+                             pair_engine=engine_id)
     table = Dd.HashTable(S * world, dev) if world > 1 else None
 
     stages = ["draw", "xt_count", "pairs", "unique", "exchange"]
@@ -209,15 +215,20 @@ def main():
     }
     if want_pairs:
         tops = pair_ops / (stage_ms["pairs"] * 1e-3) / 1e12 if stage_ms["pairs"] else 0.0
-        kernels["pairs_mfma"] = {"ms": stage_ms["pairs"], "TOPs": tops, "mfma_util": tops * 1e12 / I8_MFMA_PEAK}
+        kernels["pairs_mfma"] = {"ms": stage_ms["pairs"], "engine": args.pair_engine, "operands": engine_desc,
+                                 "TOPs": tops, "ops_per_launch": pair_ops,
+                                 "mfma_util": tops * 1e12 / engine_peak, "peak_TOPs": engine_peak / 1e12,
+                                 "int8_peak_equiv": tops * 1e12 / I8_MFMA_PEAK,
+                                 "note": "ops = S*n*(n+1) (upper triangle incl. diagonal of 2*S*n^2); "
+                                         "ms includes the partial-block reduce kernel"}
     if world > 1:
         kernels["exchange"] = {"ms": stage_ms["exchange"]}
     dominant = max(("draw", "xt_count", "pairs", "unique"), key=lambda s: stage_ms[s])
     pmc = load_pmc_traffic(args.config)
     if dominant == "pairs":
         ach = pair_ops / (stage_ms["pairs"] * 1e-3) / 1e12
-        roof = {"kernel": "pair_mfma_kernel", "bound": "mfma", "achieved": ach, "peak": I8_MFMA_PEAK / 1e12,
-                "unit": "TFLOP/s", "frac": ach * 1e12 / I8_MFMA_PEAK, "traffic": None}
+        roof = {"kernel": "pair_mfma_kernel", "bound": "mfma", "achieved": ach, "peak": engine_peak / 1e12,
+                "unit": "TFLOP/s", "frac": ach * 1e12 / engine_peak, "traffic": None}
     else:
         name = {"draw": "draw_kernel", "xt_count": "xt_count_kernel", "unique": "unique_kernel"}[dominant]
         b = {"draw": draw_bytes, "xt_count": xt_bytes, "unique": uniq_bytes}[dominant]
@@ -243,7 +254,7 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "int32/u64 (integer draw), i8 MFMA -> i32 pairs",
+        "dtype": "int32/u64 (integer draw), %s MFMA -> exact int pairs" % args.pair_engine,
         "data": "synthetic instance %s (tests/golden/instances), Philox seed %d" % (inst_dir, args.seed),
         "config": {"workload": "%s: %d LEGACY panels/GPU/step, k=%d, n=%d, C=%d, F=%d, counts+%sunique" % (
             args.config, S, k, n, enc.C, enc.F, "pairs+" if want_pairs else ""),
@@ -253,6 +264,7 @@ def main():
     }
     if want_pairs:
         result["xtx_mfma_util"] = kernels["pairs_mfma"]["mfma_util"]
+        result["xtx_int8_peak_equiv"] = kernels["pairs_mfma"]["int8_peak_equiv"]
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cb = cpu_baseline(inst_dir, k, args.seed, args.cpu_seconds, want_pairs)
         result["cpu_baseline"] = cb

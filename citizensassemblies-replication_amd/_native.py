@@ -28,6 +28,9 @@ CSA_WANT_COUNTS = 0x2
 CSA_WANT_PAIRS = 0x4
 CSA_WANT_UNIQUE = 0x8
 
+CSA_PAIR_FP4 = 0
+CSA_PAIR_I8 = 1
+
 # every symbol include/csa_legacy.h declares, with its ctypes signature
 _P = ctypes.c_void_p
 _I32 = ctypes.c_int32
@@ -47,6 +50,8 @@ SIGNATURES = {
     "csa_draw_async": (ctypes.c_int, [_P, _I32, _U64, _U64, _U64, _U32, _P, _P, _P, _P, _P, _P]),
     "csa_xt_pad": (_I32, [_I32]),
     "csa_transpose_count_async": (ctypes.c_int, [_P, _U64, _I32, _P, _P, _P]),
+    "csa_pair_scratch_bytes": (_U64, [_I32, _U64, _U32]),
+    "csa_pair_counts_ex_async": (ctypes.c_int, [_P, _U64, _I32, _P, _U32, _P, _U64, _P]),
     "csa_pair_counts_async": (ctypes.c_int, [_P, _U64, _I32, _P, _P]),
     "csa_unique_async": (ctypes.c_int, [_P, _P, _U64, _I32, _P, _U64, _P, _P]),
     "csa_unique_hashes_async": (ctypes.c_int, [_P, _U64, _U32, _U32, _P, _U64, _P, _P]),

@@ -8,8 +8,10 @@
 //                        (seed, panel, attempt, step).               legacy.py:47-200
 //   xt_count_kernel      64x64 bit-matrix transpose of the packed panels + per-person
 //                        popcounts (Counter.update, analysis.py:179,187).  HBM-bound.
-//   pair_mfma_kernel     X^T X on v_mfma_i32_32x32x32_i8, panels as the K dimension,
-//                        upper-triangular 128x128 tiles, split-K, int64 atomics
+//   pair_mfma_kernel     X^T X on MFMA, panels as the K dimension: fp4 (e2m1, exact 0/1
+//                        products, f32 accumulation) or int8 (v_mfma_i32_32x32x32_i8);
+//                        upper-triangular 256x256 blocks, split-K, int32 partial tiles +
+//                        pair_reduce_kernel
 //                        (PairHistogram.add_portfolio_of_panels_to_histogram, analysis.py:90-95).
 //   unique_kernel        open-addressing table of panel indices keyed by a 128-bit panel
 //                        hash, exact full-bitmask compare (found_panels, analysis.py:171,186).
@@ -17,6 +19,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <type_traits>
 #include <cstdlib>
 #include <cstdarg>
 #include <cstdio>
@@ -578,19 +581,36 @@ __global__ __launch_bounds__(kXtThreads) void xt_count_kernel(const uint64_t *__
 }
 
 // ------------------------------------------------------------------------------------------
-// Pair counts: X^T X on int8 MFMA
+// Pair counts: X^T X on MFMA (PairHistogram.add_portfolio_of_panels_to_histogram, analysis.py:90-95)
 // ------------------------------------------------------------------------------------------
+// Panels are the K dimension; one 64-bit XT word = one agent over 64 panels = 64 k-values.
+// Two engines share the tiling (256 x 256 upper-triangular output block per 512-thread
+// workgroup, 8 waves of 128 rows x 64 columns, two waves per SIMD):
+//   CSA_PAIR_FP4  v_mfma_scale_f32_32x32x64_f8f6f4 with e2m1 operands (scale 2^0): one MFMA
+//                 per 32x32 tile per word (K = 64), f32 accumulation.  A k-bit becomes an fp4
+//                 nibble with one set bit at position 0 / 1 / 2 (0.5 / 1.0 / 2.0); A and B put
+//                 the same bit at complementary positions, so every product of two set bits is
+//                 exactly 1.0 and the accumulators hold exact integer counts while < 2^24
+//                 (enforced per split on the host).  4-5 VALU per 32 operand bits.
+//   CSA_PAIR_I8   v_mfma_i32_32x32x32_i8 with 0/1 bytes, int32 accumulation: two MFMAs per
+//                 word (K = 32 each), 16 VALU per 32 operand bits.
+// Per KB-block stage the workgroup stages the packed words of its 256 rows + 256 columns in
+// LDS (double-buffered, one barrier per KB blocks); each wave expands its own fragments in
+// registers.  Splits of the panel blocks write int32 partial tiles (plain coalesced stores)
+// that pair_reduce_kernel sums into the int64 output, or (no scratch) int64 atomics.
 typedef int v4i __attribute__((ext_vector_type(4)));
+typedef int v8i __attribute__((ext_vector_type(8)));
 typedef int v16i __attribute__((ext_vector_type(16)));
+typedef float v16f __attribute__((ext_vector_type(16)));
 
-constexpr int kPairBlock = 256;   // output tile per workgroup: 8 waves of 128 rows x 64 columns
+constexpr int kPairBlock = 256;   // output block per workgroup
 constexpr int kPairThreads = 512;
+constexpr int kPairKB = 4;        // 64-panel blocks staged per barrier
 
-// MFMA operand fragment (k-half ks, lane half h) of one XT word w: dword q holds the four bits
-// 4h+q, 4h+q+8, 4h+q+16, 4h+q+24 of the 32-bit half ks as int8 0/1 values (2 VALU per dword).
-// Any fixed bit->k placement works because A and B fragments use the same one (the k order
-// cancels in the sum over k), and the four (ks, h) fragments cover all 64 panels once.
-__device__ __forceinline__ v4i xt_frag(uint64_t w, int ks, int h) {
+// int8 fragment (k-half ks, lane half h) of one XT word: dword q holds bits 4h+q, 4h+q+8,
+// 4h+q+16, 4h+q+24 of the 32-bit half ks as 0/1 bytes.  Any fixed bit -> k placement works
+// because A and B use the same one (the k order cancels in the sum over k).
+__device__ __forceinline__ v4i i8_frag(uint64_t w, int ks, int h) {
     const uint32_t x = (uint32_t)(w >> (32 * ks));
     v4i r;
 #pragma unroll
@@ -598,30 +618,59 @@ __device__ __forceinline__ v4i xt_frag(uint64_t w, int ks, int h) {
     return r;
 }
 
-// X^T X over panel blocks [kb0, kb1) for one 256 x 256 upper-triangular output block.
-// Per 64-panel step the 512 threads stage the packed XT words of the block's 256 rows and 256
-// columns in LDS (4 KiB, double-buffered, one barrier per step); wave (wr, wc) reads the words
-// of its 128 rows and 64 columns, expands them into int8 fragments in registers and issues
-// 2 x 4 x 2 v_mfma_i32_32x32x32_i8 (two waves per SIMD interleave expansion and MFMA).
-__global__ __launch_bounds__(kPairThreads) void pair_mfma_kernel(const uint64_t *__restrict__ xt,
-                                                                 uint64_t nblk, int n, int npad,
-                                                                 int nbt, int nsplit,
-                                                                 int64_t *__restrict__ pairs) {
-    __shared__ uint64_t words[2][2 * kPairBlock];
-    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-    const int item = blockIdx.x;
-    const int tri = item / nsplit, split = item - tri * nsplit;
-    int bi = 0, rem = tri;
+// fp4 fragments of the 32 bits x = word >> 32h (lane half h covers k = 32h .. 32h+31):
+// bit 4i+p of x goes to nibble i of dword p (A: positions 0,1,2,2 -> 0.5,1,2,2;
+// B: positions 2,1,0,0 -> 2,1,0.5,0.5).
+__device__ __forceinline__ v8i f4_frag_a(uint64_t w, int h) {
+    const uint32_t x = (uint32_t)(w >> (32 * h));
+    v8i r;
+    r[0] = (int)(x & 0x11111111u);
+    r[1] = (int)(x & 0x22222222u);
+    r[2] = (int)(x & 0x44444444u);
+    r[3] = (int)((x >> 1) & 0x44444444u);
+    r[4] = r[5] = r[6] = r[7] = 0;  // fp4 operands use 4 registers
+    return r;
+}
+__device__ __forceinline__ v8i f4_frag_b(uint64_t w, int h) {
+    const uint32_t x = (uint32_t)(w >> (32 * h));
+    v8i r;
+    r[0] = (int)((x << 2) & 0x44444444u);
+    r[1] = (int)(x & 0x22222222u);
+    r[2] = (int)((x >> 2) & 0x11111111u);
+    r[3] = (int)((x >> 3) & 0x11111111u);
+    r[4] = r[5] = r[6] = r[7] = 0;
+    return r;
+}
+
+__device__ __forceinline__ void tri_block(int tri, int nbt, int &bi, int &bj) {
+    bi = 0;
+    int rem = tri;
     while (rem >= nbt - bi) {
         rem -= nbt - bi;
         ++bi;
     }
-    const int bj = bi + rem;
+    bj = bi + rem;
+}
+
+template <bool FP4, bool PARTIAL>
+__global__ __launch_bounds__(kPairThreads) void pair_mfma_kernel(const uint64_t *__restrict__ xt,
+                                                                 uint64_t nblk, int n, int npad,
+                                                                 int nbt, int nsplit,
+                                                                 int64_t *__restrict__ pairs,
+                                                                 int32_t *__restrict__ part) {
+    constexpr int KB = kPairKB;
+    __shared__ uint64_t words[2][KB][2 * kPairBlock];
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    const int item = blockIdx.x;
+    const int tri = item / nsplit, split = item - tri * nsplit;
+    int bi, bj;
+    tri_block(tri, nbt, bi, bj);
     const int I0 = bi * kPairBlock, J0 = bj * kPairBlock;
     const uint64_t per = (nblk + nsplit - 1) / nsplit;
-    const uint64_t kb0 = (uint64_t)split * per, kb1 = min(nblk, kb0 + per);
+    const uint64_t kb0 = min(nblk, (uint64_t)split * per), kb1 = min(nblk, kb0 + per);
 
-    v16i acc[4][2];
+    using acc_t = typename std::conditional<FP4, v16f, v16i>::type;
+    acc_t acc[4][2];
 #pragma unroll
     for (int a = 0; a < 4; ++a)
 #pragma unroll
@@ -632,54 +681,114 @@ __global__ __launch_bounds__(kPairThreads) void pair_mfma_kernel(const uint64_t 
     const int wr = wave >> 2, wc = wave & 3;
     const int r32 = lane & 31, h = lane >> 5;
     const int src = t < kPairBlock ? I0 + t : J0 + t - kPairBlock;  // staging role of this thread
-    uint64_t nw = 0;
-    if (kb0 < kb1) {
-        words[kb0 & 1][t] = xt[kb0 * (uint64_t)npad + src];
-        nw = xt[min(kb0 + 1, kb1 - 1) * (uint64_t)npad + src];
+    uint64_t nw[KB];
+    const uint64_t nst = (kb1 - kb0 + KB - 1) / KB;
+    auto load_stage = [&](uint64_t s) {
+#pragma unroll
+        for (int j = 0; j < KB; ++j) nw[j] = xt[min(kb0 + s * KB + j, kb1 - 1) * (uint64_t)npad + src];
+    };
+    if (nst) {
+        load_stage(0);
+#pragma unroll
+        for (int j = 0; j < KB; ++j) words[0][j][t] = nw[j];
+        if (nst > 1) load_stage(1);
     }
     __syncthreads();
-    for (uint64_t kb = kb0; kb < kb1; ++kb) {
-        const uint64_t *w = words[kb & 1];
-        uint64_t wa[4], wb[2];
+    for (uint64_t s = 0; s < nst; ++s) {
+        const int buf = (int)(s & 1);
+        const int jmax = (int)min<uint64_t>(KB, kb1 - kb0 - s * KB);
 #pragma unroll
-        for (int x = 0; x < 4; ++x) wa[x] = w[128 * wr + 32 * x + r32];
+        for (int j = 0; j < KB; ++j) {
+            if (j < jmax) {
+                const uint64_t *w = words[buf][j];
+                uint64_t wa[4], wb[2];
 #pragma unroll
-        for (int x = 0; x < 2; ++x) wb[x] = w[kPairBlock + 64 * wc + 32 * x + r32];
-        words[(kb + 1) & 1][t] = nw;  // the last step stages a duplicate nobody reads
-        nw = xt[min(kb + 2, kb1 - 1) * (uint64_t)npad + src];
+                for (int x = 0; x < 4; ++x) wa[x] = w[128 * wr + 32 * x + r32];
 #pragma unroll
-        for (int ks = 0; ks < 2; ++ks) {
-            v4i fa[4], fb[2];
+                for (int x = 0; x < 2; ++x) wb[x] = w[kPairBlock + 64 * wc + 32 * x + r32];
+                if constexpr (FP4) {
+                    v8i fa[4], fb[2];
 #pragma unroll
-            for (int x = 0; x < 4; ++x) fa[x] = xt_frag(wa[x], ks, h);
+                    for (int x = 0; x < 4; ++x) fa[x] = f4_frag_a(wa[x], h);
 #pragma unroll
-            for (int x = 0; x < 2; ++x) fb[x] = xt_frag(wb[x], ks, h);
+                    for (int x = 0; x < 2; ++x) fb[x] = f4_frag_b(wb[x], h);
 #pragma unroll
-            for (int a = 0; a < 4; ++a)
+                    for (int a = 0; a < 4; ++a)
 #pragma unroll
-                for (int b = 0; b < 2; ++b)
-                    acc[a][b] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[a], fb[b], acc[a][b], 0, 0, 0);
+                        for (int b = 0; b < 2; ++b)
+                            acc[a][b] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(
+                                fa[a], fb[b], acc[a][b], 4, 4, 0, 0x7F7F7F7F, 0, 0x7F7F7F7F);
+                } else {
+#pragma unroll
+                    for (int ks = 0; ks < 2; ++ks) {
+                        v4i fa[4], fb[2];
+#pragma unroll
+                        for (int x = 0; x < 4; ++x) fa[x] = i8_frag(wa[x], ks, h);
+#pragma unroll
+                        for (int x = 0; x < 2; ++x) fb[x] = i8_frag(wb[x], ks, h);
+#pragma unroll
+                        for (int a = 0; a < 4; ++a)
+#pragma unroll
+                            for (int b = 0; b < 2; ++b)
+                                acc[a][b] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[a], fb[b], acc[a][b], 0, 0, 0);
+                    }
+                }
+            }
+            if (j == 0) {  // hand the prefetched stage to LDS, prefetch the one after
+                if (s + 1 < nst) {
+#pragma unroll
+                    for (int jj = 0; jj < KB; ++jj) words[buf ^ 1][jj][t] = nw[jj];
+                }
+                if (s + 2 < nst) load_stage(s + 2);
+            }
         }
         __syncthreads();
     }
     // C/D layout (gfx950, dtype-independent): col = lane & 31, row = (v&3) + 8*(v>>2) + 4*(lane>>5)
-    const int rbase = I0 + 128 * wr + 4 * h;
-    const int cbase = J0 + 64 * wc + r32;
+    const int rloc = 128 * wr + 4 * h, cloc = 64 * wc + r32;
+    if constexpr (PARTIAL) {
+        int32_t *dst = part + (size_t)item * kPairBlock * kPairBlock;
 #pragma unroll
-    for (int a = 0; a < 4; ++a)
+        for (int a = 0; a < 4; ++a)
 #pragma unroll
-        for (int b = 0; b < 2; ++b) {
-            const int col = cbase + 32 * b;
+            for (int b = 0; b < 2; ++b)
 #pragma unroll
-            for (int v = 0; v < 16; ++v) {
-                const int row = rbase + 32 * a + (v & 3) + 8 * (v >> 2);
-                const int val = acc[a][b][v];
-                if (val != 0 && row < n && col < n)
-                    atomicAdd(reinterpret_cast<unsigned long long *>(pairs + (uint64_t)row * n + col),
-                              (unsigned long long)(long long)val);
+                for (int v = 0; v < 16; ++v) {
+                    const int row = rloc + 32 * a + (v & 3) + 8 * (v >> 2);
+                    dst[row * kPairBlock + cloc + 32 * b] = (int)acc[a][b][v];
+                }
+    } else {
+#pragma unroll
+        for (int a = 0; a < 4; ++a)
+#pragma unroll
+            for (int b = 0; b < 2; ++b) {
+                const int col = J0 + cloc + 32 * b;
+#pragma unroll
+                for (int v = 0; v < 16; ++v) {
+                    const int row = I0 + rloc + 32 * a + (v & 3) + 8 * (v >> 2);
+                    const int val = (int)acc[a][b][v];
+                    if (val != 0 && row < n && col < n)
+                        atomicAdd(reinterpret_cast<unsigned long long *>(pairs + (uint64_t)row * n + col),
+                                  (unsigned long long)(long long)val);
+                }
+                __builtin_amdgcn_sched_barrier(0);  // keep the atomic addresses from being hoisted (VGPR spill)
             }
-            __builtin_amdgcn_sched_barrier(0);  // keep the atomic addresses from being hoisted (VGPR spill)
-        }
+    }
+}
+
+// Sum the nsplit int32 partial tiles of every upper-triangular block into the int64 output
+// (+=; each output element is owned by exactly one thread).  HBM-bound.
+__global__ __launch_bounds__(256) void pair_reduce_kernel(const int32_t *__restrict__ part, int n, int nbt,
+                                                          int nsplit, int64_t *__restrict__ pairs) {
+    int bi, bj;
+    tri_block((int)blockIdx.y, nbt, bi, bj);
+    const int e = blockIdx.x * 256 + threadIdx.x;  // element of the 256 x 256 block
+    const int row = bi * kPairBlock + (e >> 8), col = bj * kPairBlock + (e & 255);
+    if (row >= n || col >= n) return;
+    const int32_t *p = part + (size_t)blockIdx.y * nsplit * kPairBlock * kPairBlock + e;
+    int64_t acc = 0;
+    for (int k = 0; k < nsplit; ++k) acc += p[(size_t)k * kPairBlock * kPairBlock];
+    if (acc) pairs[(size_t)row * n + col] += acc;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1064,25 +1173,77 @@ int csa_transpose_count_async(const uint64_t *d_panels, uint64_t n_panels, int32
     return CSA_OK;
 }
 
-int csa_pair_counts_async(const uint64_t *d_xt, uint64_t n_blocks, int32_t n, int64_t *d_pairs, void *stream) {
+namespace {
+struct PairPlan {
+    int npad, nbt, ntri, nsplit;
+};
+
+// one 512-thread workgroup per CU (two waves per SIMD): fill the CUs once, keep >= 8 panel
+// blocks per split, and keep every split below the accumulator's exact range (f32: 2^24)
+int pair_plan(int32_t n, uint64_t n_blocks, uint32_t engine, PairPlan &p) {
+    if (engine != CSA_PAIR_FP4 && engine != CSA_PAIR_I8) return fail(CSA_E_INVALID, "pairs: unknown engine %u", engine);
+    p.npad = csa_xt_pad(n);
+    p.nbt = p.npad / kPairBlock;
+    p.ntri = p.nbt * (p.nbt + 1) / 2;
+    int cus = 256;
+    int dev = 0;
+    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    uint64_t ns = std::max(1, cus / p.ntri);
+    ns = std::min<uint64_t>(ns, std::max<uint64_t>(1, n_blocks / 8));
+    const uint64_t exact_blocks = engine == CSA_PAIR_FP4 ? (1ull << 24) / 64 : (1ull << 31) / 64;
+    ns = std::max<uint64_t>(ns, (n_blocks + exact_blocks - 1) / exact_blocks);
+    if (ns > (1u << 20)) return fail(CSA_E_UNSUPPORTED, "pairs: too many panel blocks per call");
+    p.nsplit = (int)ns;
+    return CSA_OK;
+}
+}  // namespace
+
+uint64_t csa_pair_scratch_bytes(int32_t n, uint64_t n_blocks, uint32_t engine) {
+    PairPlan p;
+    if (n <= 0 || n_blocks == 0 || pair_plan(n, n_blocks, engine, p)) return 0;
+    return (uint64_t)p.ntri * p.nsplit * kPairBlock * kPairBlock * sizeof(int32_t);
+}
+
+int csa_pair_counts_ex_async(const uint64_t *d_xt, uint64_t n_blocks, int32_t n, int64_t *d_pairs,
+                             uint32_t engine, void *d_scratch, uint64_t scratch_bytes, void *stream) {
     if (n <= 0 || !d_xt || !d_pairs) return fail(CSA_E_INVALID, "pairs: bad arguments");
     if (n_blocks == 0) return CSA_OK;
-    if (n_blocks * 64 >= (1ull << 31)) return fail(CSA_E_UNSUPPORTED, "pairs: > 2^31 panels per call");
-    const int npad = csa_xt_pad(n), nbt = npad / kPairBlock;
-    const int ntri = nbt * (nbt + 1) / 2;
-    // one 512-thread workgroup per CU (128 accumulator registers per wave): fill the 256 CUs once,
-    // keeping >= 8 panel blocks per split
-    int cus = 256;
-    {
-        int dev = 0;
-        if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    PairPlan p;
+    int rc = pair_plan(n, n_blocks, engine, p);
+    if (rc) return rc;
+    const bool partial = d_scratch != nullptr;
+    if (partial && scratch_bytes < csa_pair_scratch_bytes(n, n_blocks, engine))
+        return fail(CSA_E_INVALID, "pairs: scratch of %llu B < csa_pair_scratch_bytes = %llu B",
+                    (unsigned long long)scratch_bytes, (unsigned long long)csa_pair_scratch_bytes(n, n_blocks, engine));
+    const dim3 grid(p.ntri * p.nsplit), block(kPairThreads);
+    int32_t *part = static_cast<int32_t *>(d_scratch);
+    const hipStream_t st = (hipStream_t)stream;
+    if (engine == CSA_PAIR_FP4) {
+        if (partial)
+            hipLaunchKernelGGL((pair_mfma_kernel<true, true>), grid, block, 0, st, d_xt, n_blocks, n, p.npad, p.nbt,
+                               p.nsplit, d_pairs, part);
+        else
+            hipLaunchKernelGGL((pair_mfma_kernel<true, false>), grid, block, 0, st, d_xt, n_blocks, n, p.npad, p.nbt,
+                               p.nsplit, d_pairs, part);
+    } else {
+        if (partial)
+            hipLaunchKernelGGL((pair_mfma_kernel<false, true>), grid, block, 0, st, d_xt, n_blocks, n, p.npad, p.nbt,
+                               p.nsplit, d_pairs, part);
+        else
+            hipLaunchKernelGGL((pair_mfma_kernel<false, false>), grid, block, 0, st, d_xt, n_blocks, n, p.npad,
+                               p.nbt, p.nsplit, d_pairs, part);
     }
-    int nsplit = std::max(1, cus / ntri);
-    nsplit = (int)std::min<uint64_t>((uint64_t)nsplit, std::max<uint64_t>(1, n_blocks / 8));
-    hipLaunchKernelGGL(pair_mfma_kernel, dim3(ntri * nsplit), dim3(kPairThreads), 0, (hipStream_t)stream, d_xt,
-                       n_blocks, n, npad, nbt, nsplit, d_pairs);
     HIPCHK(hipGetLastError());
+    if (partial) {
+        hipLaunchKernelGGL(pair_reduce_kernel, dim3(kPairBlock, p.ntri), dim3(256), 0, st, part, n, p.nbt, p.nsplit,
+                           d_pairs);
+        HIPCHK(hipGetLastError());
+    }
     return CSA_OK;
+}
+
+int csa_pair_counts_async(const uint64_t *d_xt, uint64_t n_blocks, int32_t n, int64_t *d_pairs, void *stream) {
+    return csa_pair_counts_ex_async(d_xt, n_blocks, n, d_pairs, CSA_PAIR_FP4, nullptr, 0, stream);
 }
 
 int csa_unique_async(const uint64_t *d_hashes, const uint64_t *d_panels, uint64_t n_panels, int32_t W,
@@ -1171,7 +1332,13 @@ int csa_legacy_sample(csa_instance *I, int32_t k, uint64_t seed, uint64_t panel_
     if ((rc = read_status(status.p, st, hs))) return rc;
     if ((rc = csa_status_decode(hs))) return rc;
     if (counts.p && (rc = csa_transpose_count_async(panels.p, n_panels, n, xt.p, counts.p, st))) return rc;
-    if (pairs.p && (rc = csa_pair_counts_async(xt.p, nblk, n, pairs.p, st))) return rc;
+    if (pairs.p) {
+        DevBuf<int32_t> scratch;
+        const uint64_t sb = csa_pair_scratch_bytes(n, nblk, CSA_PAIR_FP4);
+        if ((rc = dalloc(&scratch.p, sb / sizeof(int32_t)))) return rc;
+        if ((rc = csa_pair_counts_ex_async(xt.p, nblk, n, pairs.p, CSA_PAIR_FP4, scratch.p, sb, st))) return rc;
+        HIPCHK(hipStreamSynchronize(st));  // scratch is freed at scope exit
+    }
     if (want_unique && (rc = csa_unique_async(hashes.p, panels.p, n_panels, W, table.p, slots, uniq.p, st)))
         return rc;
     if (flags & CSA_WANT_PANELS)

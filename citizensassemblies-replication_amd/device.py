@@ -6,7 +6,8 @@ RCCL collectives; every kernel is the hand-written HIP in csrc/.  One
 
     draw_kernel        panels [panel_begin, panel_begin+S) -> packed bitmasks + 128-bit hashes
     xt_count_kernel    bitmasks -> transposed panel-indicator bits + per-person counts (+=)
-    pair_mfma_kernel   transposed bits -> pair counts X^T X (+=)        (if want_pairs)
+    pair_mfma_kernel   transposed bits -> int32 partial blocks of X^T X on fp4 (default) or
+    pair_reduce_kernel   int8 MFMA -> pair counts (+=)                  (if want_pairs)
     unique_kernel      hashes (+ bitmasks) -> distinct-panel count (+=)  (if want_unique)
 
 Buffers are allocated once for the largest shard and reused across runs, so a
@@ -25,13 +26,14 @@ def _stream_ptr(stream):
 
 class DevicePipeline:
     def __init__(self, enc, k, max_panels, want_pairs=True, want_unique=True, want_attempts=False,
-                 device=None, stream=None):
+                 device=None, stream=None, pair_engine=N.CSA_PAIR_FP4):
         self.enc = enc
         self.k = int(k)
         self.device = torch.device(device or "cuda")
         self.stream = stream or torch.cuda.current_stream(self.device)
         self.want_pairs = want_pairs
         self.want_unique = want_unique
+        self.pair_engine = int(pair_engine)
         S = int(max_panels)
         self.max_panels = S
         n, W = enc.n, enc.W
@@ -52,6 +54,8 @@ class DevicePipeline:
             self.counts = torch.zeros(n, dtype=torch.int64, device=dev)
             self.xt = torch.empty(nblk * self.npad, dtype=u64, device=dev) if want_pairs else None
             self.pairs = torch.zeros(n * n, dtype=torch.int64, device=dev) if want_pairs else None
+            sb = int(L.csa_pair_scratch_bytes(max(n, 1), max(nblk, 1), self.pair_engine)) if want_pairs else 0
+            self.pair_scratch = torch.empty((sb + 3) // 4, dtype=torch.int32, device=dev) if want_pairs else None
             self.table = torch.empty(slots, dtype=u64, device=dev) if want_unique else None
             self.unique = torch.zeros(1, dtype=torch.int64, device=dev)
         _ = enc.handle  # upload the instance on this device
@@ -78,8 +82,13 @@ class DevicePipeline:
                                                   N.ptr(self.counts), _stream_ptr(self.stream)))
 
     def pair_counts(self, S):
-        N.check(N.lib().csa_pair_counts_async(N.ptr(self.xt), (int(S) + 63) // 64, self.enc.n,
-                                              N.ptr(self.pairs), _stream_ptr(self.stream)))
+        nblk = (int(S) + 63) // 64
+        L = N.lib()
+        need = int(L.csa_pair_scratch_bytes(self.enc.n, nblk, self.pair_engine))
+        assert need <= self.pair_scratch.numel() * 4
+        N.check(L.csa_pair_counts_ex_async(N.ptr(self.xt), nblk, self.enc.n, N.ptr(self.pairs), self.pair_engine,
+                                           N.ptr(self.pair_scratch), self.pair_scratch.numel() * 4,
+                                           _stream_ptr(self.stream)))
 
     def unique_count(self, S):
         N.check(N.lib().csa_unique_async(N.ptr(self.hashes), N.ptr(self.panels), int(S), self.enc.W,

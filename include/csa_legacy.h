@@ -132,10 +132,24 @@ int32_t csa_xt_pad(int32_t n);
 int csa_transpose_count_async(const uint64_t *d_panels, uint64_t n_panels, int32_t n,
                               uint64_t *d_xt, int64_t *d_counts, void *stream);
 
-/* Pair counts X^T X on int8 MFMA (v_mfma_i32_32x32x32_i8), upper-triangular
- * tiles, split over panel blocks.  d_xt as produced above (n_blocks =
- * ceil(n_panels/64)); d_pairs (n*n int64, row-major) is ACCUMULATED (+=) for
- * i <= j (lower triangle unspecified).  Exact for n_panels < 2^31 per call. */
+/* Pair counts X^T X on MFMA, upper-triangular 256x256 blocks split over panel
+ * blocks (replaces PairHistogram.add_portfolio_of_panels_to_histogram,
+ * analysis.py:90-95, summed over all panels).  d_xt as produced above
+ * (n_blocks = ceil(n_panels/64)); d_pairs (n*n int64, row-major) is
+ * ACCUMULATED (+=) for i <= j (lower triangle unspecified).  Exact for any
+ * n_blocks (each split stays inside its accumulator's exact integer range).
+ * engine: CSA_PAIR_FP4 = v_mfma_scale_f32_32x32x64_f8f6f4 on e2m1 0/1-products
+ * (f32 accumulation, exact below 2^24 per split); CSA_PAIR_I8 =
+ * v_mfma_i32_32x32x32_i8 (int32 accumulation).  With d_scratch (at least
+ * csa_pair_scratch_bytes bytes of device memory) each split writes an int32
+ * partial block and a reduce kernel sums them; with d_scratch == NULL the
+ * splits add into d_pairs with int64 atomics.  csa_pair_counts_async =
+ * engine FP4, no scratch. */
+#define CSA_PAIR_FP4 0u
+#define CSA_PAIR_I8 1u
+uint64_t csa_pair_scratch_bytes(int32_t n, uint64_t n_blocks, uint32_t engine);
+int csa_pair_counts_ex_async(const uint64_t *d_xt, uint64_t n_blocks, int32_t n, int64_t *d_pairs,
+                             uint32_t engine, void *d_scratch, uint64_t scratch_bytes, void *stream);
 int csa_pair_counts_async(const uint64_t *d_xt, uint64_t n_blocks, int32_t n, int64_t *d_pairs,
                           void *stream);
 

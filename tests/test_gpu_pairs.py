@@ -1,0 +1,87 @@
+"""GPU parity of the X^T X pair-count kernels (PairHistogram, analysis.py:68-98) through the C ABI.
+
+Both MFMA engines (fp4 e2m1 with f32 accumulation, int8 with int32
+accumulation) and both epilogues (int32 partial blocks + reduce kernel, int64
+atomics) against an exact CPU popcount restatement on the same packed
+transposed bits.  Bar: bit-exact.
+"""
+import numpy as np
+import pytest
+
+from conftest import pkg
+
+pytestmark = pytest.mark.gpu
+
+
+def _popcount64(a):
+    return np.unpackbits(a.view(np.uint8)).sum(dtype=np.int64)
+
+
+def _cpu_pairs(xt, n, npad, rows=None):
+    """Exact pair counts from the packed transposed bits xt[b, p] (uint64)."""
+    X = np.unpackbits(xt[:, :n].copy().view(np.uint8).reshape(xt.shape[0], n, 8), axis=2, bitorder="little")
+    X = X.transpose(0, 2, 1).reshape(-1, n).astype(np.float64)    # panels x agents
+    return np.rint(X.T @ X).astype(np.int64)                      # BLAS; exact below 2^53
+
+
+def _run(xt_np, n, engine, scratch):
+    import torch
+    N = pkg("_native")
+    L = N.lib()
+    nblk = xt_np.shape[0]
+    xt = torch.from_numpy(xt_np.view(np.int64).copy()).cuda()
+    pairs = torch.zeros(n * n, dtype=torch.int64, device="cuda")
+    sb = int(L.csa_pair_scratch_bytes(n, nblk, engine))
+    scr = torch.empty((sb + 3) // 4, dtype=torch.int32, device="cuda") if scratch else None
+    N.check(L.csa_pair_counts_ex_async(N.ptr(xt), nblk, n, N.ptr(pairs), engine, N.ptr(scr),
+                                       sb if scratch else 0, None))
+    torch.cuda.synchronize()
+    return pairs.cpu().numpy().reshape(n, n)
+
+
+@pytest.mark.parametrize("n,S", [(20, 10000), (200, 70000), (300, 6400), (1727, 20000), (2000, 3000)])
+@pytest.mark.parametrize("engine,scratch", [(0, True), (0, False), (1, True), (1, False)])
+def test_pair_engines_exact(gpu_available, n, S, engine, scratch):
+    N = pkg("_native")
+    npad = int(N.lib().csa_xt_pad(n))
+    nblk = (S + 63) // 64
+    rng = np.random.default_rng(n * 7 + S)
+    dens = rng.integers(0, 2 ** 64, size=(nblk, npad), dtype=np.uint64)
+    xt = dens & rng.integers(0, 2 ** 64, size=(nblk, npad), dtype=np.uint64)   # ~25% density
+    xt[:, 0] = np.uint64(2 ** 64 - 1)                                          # a dense agent
+    if S % 64:                                                                 # ragged last block
+        xt[-1, :] &= np.uint64((1 << (S % 64)) - 1)
+    got = _run(xt, n, engine, scratch)
+    ref = _cpu_pairs(xt, n, npad)
+    iu = np.triu_indices(n)
+    assert np.array_equal(got[iu], ref[iu])
+
+
+def test_pair_fp4_exact_beyond_f32_range(gpu_available):
+    """> 2^24 panels in one call with few output blocks: every split must stay below 2^24."""
+    import torch
+    N = pkg("_native")
+    n = 6000                                   # 24 x 24 blocks -> 300 triangle blocks, 1 split by occupancy
+    npad = int(N.lib().csa_xt_pad(n))
+    nblk = (1 << 18) + 5                       # 2^24 + 320 panels
+    S = nblk * 64
+    # agents 0, 1, n-1 dense-ish; everything else zero (cheap to build, exact counts known)
+    xt = torch.zeros(nblk, npad, dtype=torch.int64, device="cuda")
+    xt[:, 0] = -1                              # all ones
+    xt[:, n - 1] = -1
+    g = torch.Generator(device="cuda").manual_seed(5)
+    xt[:, 1] = torch.randint(-2 ** 63, 2 ** 63 - 1, (nblk,), device="cuda", generator=g)
+    pairs = torch.zeros(n * n, dtype=torch.int64, device="cuda")
+    L = N.lib()
+    sb = int(L.csa_pair_scratch_bytes(n, nblk, N.CSA_PAIR_FP4))
+    assert sb >= 2 * 300 * 256 * 256 * 4       # the exactness guard forced >= 2 splits
+    scr = torch.empty(sb // 4, dtype=torch.int32, device="cuda")
+    N.check(L.csa_pair_counts_ex_async(N.ptr(xt), nblk, n, N.ptr(pairs), N.CSA_PAIR_FP4, N.ptr(scr), sb, None))
+    torch.cuda.synchronize()
+    P = pairs.view(n, n)
+    c1 = int(_popcount64(xt[:, 1].cpu().numpy()))
+    assert int(P[0, 0]) == S
+    assert int(P[0, n - 1]) == S
+    assert int(P[n - 1, n - 1]) == S
+    assert int(P[0, 1]) == c1 and int(P[1, 1]) == c1 and int(P[1, n - 1]) == c1
+    assert int(P[2, 3]) == 0 and int(P[0, 2]) == 0
