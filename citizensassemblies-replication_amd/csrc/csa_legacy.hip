@@ -111,6 +111,7 @@ struct DrawArgs {
     const uint64_t *featmask;  // F x Ws, Ws = W | 1 (odd stride: conflict-free lane-f reads)
     const int32_t *fmin, *fmax, *sel0, *rem0;
     const uint64_t *present0;  // W
+    const uint32_t *pmask;     // n person feature masks (bit f = holds feature f; F <= 32) or null
     int32_t n, F, W, Ws, k;
     uint32_t max_attempts, attempt_base;
     int32_t single;            // 1: exactly one attempt, no min-quota check, write final state
@@ -138,10 +139,12 @@ __device__ __forceinline__ int dpp(int old, int v) {
 // butterfly partner at level LVL: quad xor1, quad xor2, half-row mirror, row mirror, xor16, xor32
 template <int LVL>
 __device__ __forceinline__ int partner(int v) {
-    if constexpr (LVL == 0) return dpp<0xB1>(v, v);
-    else if constexpr (LVL == 1) return dpp<0x4E>(v, v);
-    else if constexpr (LVL == 2) return dpp<0x141>(v, v);
-    else if constexpr (LVL == 3) return dpp<0x140>(v, v);
+    // every source lane of these patterns is valid, so bound_ctrl / old are irrelevant; (0, bc=1)
+    // lets the compiler fold the DPP move into the consuming VALU op
+    if constexpr (LVL == 0) return dpp<0xB1, 0xF, true>(0, v);
+    else if constexpr (LVL == 1) return dpp<0x4E, 0xF, true>(0, v);
+    else if constexpr (LVL == 2) return dpp<0x141, 0xF, true>(0, v);
+    else if constexpr (LVL == 3) return dpp<0x140, 0xF, true>(0, v);
     else if constexpr (LVL == 4) return __shfl_xor(v, 16);
     else return __shfl_xor(v, 32);
 }
@@ -519,6 +522,30 @@ __global__ __launch_bounds__(kDrawThreads, draw_occupancy(FPL, WPL)) void draw_k
     }
 }
 
+#include "draw_batch.inc"
+
+// 128-bit panel hashes (the draw_kernel's in-kernel hash, for the batch kernel's panels): a
+// quad of lanes per panel, words glane, glane+4, ... (coalesced within the quad), quad sum.
+__global__ __launch_bounds__(256) void panel_hash_kernel(const uint64_t *__restrict__ panels, uint64_t S, int W,
+                                                         uint64_t *__restrict__ hashes) {
+    const uint64_t i = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 2;
+    const int q = threadIdx.x & 3;
+    uint64_t h1 = 0, h2 = 0;
+    if (i < S) {
+        for (int w = q; w < W; w += 4) {
+            const uint64_t pk = panels[i * W + w];
+            h1 += fmix_a(pk ^ ((uint64_t)w * 0x9E3779B97F4A7C15ull));
+            h2 += fmix_b(pk + ((uint64_t)w + 1) * 0xD6E8FEB86659FD93ull);
+        }
+    }
+    h1 = group_sum64<0, 2>(h1);
+    h2 = group_sum64<0, 2>(h2);
+    if (i < S && q == 0) {
+        hashes[2 * i] = h1;
+        hashes[2 * i + 1] = h2;
+    }
+}
+
 // ------------------------------------------------------------------------------------------
 // Bit transpose + per-person counts
 // ------------------------------------------------------------------------------------------
@@ -837,7 +864,9 @@ struct csa_instance {
     uint64_t *d_featmask = nullptr;
     int32_t *d_fmin = nullptr, *d_fmax = nullptr, *d_sel0 = nullptr, *d_rem0 = nullptr;
     uint64_t *d_present0 = nullptr;
+    uint32_t *d_pmask = nullptr;  // n person feature masks (F <= 32 only)
     int32_t max_abs = 0;  // max |fmin| / |sel0| bound for the cross-multiplication range check
+    bool zero_max_min = false;  // some feature has max 0 and min > 0 (draw_batch_kernel excludes it)
 };
 
 namespace {
@@ -870,6 +899,7 @@ int check_k(const csa_instance *I, int32_t k) {
 
 struct DrawConfig {
     int G = 16, FPL = 1, WPL = 1;
+    bool batch = false;  // draw_batch_kernel (small groups) instead of draw_kernel
     const void *fn = nullptr;
 };
 
@@ -900,26 +930,55 @@ const void *draw_fn_fw(int fpl, int wpl) {
     }
 }
 
+template <int G, int FPL>
+const void *batch_fn_w(int wpl) {
+    switch (wpl) {
+        case 1: return reinterpret_cast<const void *>(&draw_batch_kernel<G, FPL, 1>);
+        case 2: return reinterpret_cast<const void *>(&draw_batch_kernel<G, FPL, 2>);
+        case 4: return reinterpret_cast<const void *>(&draw_batch_kernel<G, FPL, 4>);
+        case 8: return reinterpret_cast<const void *>(&draw_batch_kernel<G, FPL, 8>);
+        default: return nullptr;
+    }
+}
+
+template <int G>
+const void *batch_fn(int fpl, int wpl) {
+    switch (fpl) {
+        case 1: return batch_fn_w<G, 1>(wpl);
+        case 2: return batch_fn_w<G, 2>(wpl);
+        case 4: return batch_fn_w<G, 4>(wpl);
+        case 8: if constexpr (G == 4) return batch_fn_w<G, 8>(wpl); else return nullptr;
+        default: return nullptr;
+    }
+}
+
 int pow2_ceil_int(int x) {
     int p = 1;
     while (p < x) p <<= 1;
     return p;
 }
 
-// Batch draws: G = 16 lanes per panel (4 panels per wavefront) unless the instance needs more
-// lanes; CSA_DRAW_GROUP=16|64 overrides (benchmarking).  Pick-order / single-attempt draws
-// (general mode) use the G = 64 kernels.
+// Batch draws: draw_batch_kernel with G = 4 lanes per panel (16 panels per wavefront) when the
+// instance fits (F <= 32, W <= 32), else draw_kernel with G = 16 (F <= 64) or 64.
+// CSA_DRAW_GROUP=4|8|16|64 overrides (benchmarking).  Pick-order / single-attempt draws
+// (general mode) use the G = 64 draw_kernel.
 int pick_draw_config(const csa_instance *I, bool general, DrawConfig &c) {
-    int G = (!general && I->F <= 64 && I->W <= 256) ? 16 : 64;
+    const bool small = I->F <= 32 && I->d_pmask && !I->zero_max_min && I->n <= 16384;
+    int G = general ? 64 : (small && I->W <= 32) ? 4 : (I->F <= 64 && I->W <= 256) ? 16 : 64;
     if (const char *e = getenv("CSA_DRAW_GROUP")) {
         const int g = atoi(e);
-        if (!general && (g == 16 || g == 64)) G = g;
+        if (!general && (g == 16 || g == 64 || (small && (g == 4 || g == 8)))) G = g;
     }
     c.G = G;
+    c.batch = G <= 8;
     c.FPL = pow2_ceil_int((I->F + G - 1) / G);
     c.WPL = pow2_ceil_int(std::max(1, (I->W + G - 1) / G));
     if (general)
         c.fn = draw_fn_fw<64, true>(c.FPL, c.WPL);
+    else if (G == 4)
+        c.fn = batch_fn<4>(c.FPL, c.WPL);
+    else if (G == 8)
+        c.fn = batch_fn<8>(c.FPL, c.WPL);
     else
         c.fn = G == 16 ? draw_fn_fw<16, false>(c.FPL, c.WPL) : draw_fn_fw<64, false>(c.FPL, c.WPL);
     if (!c.fn)
@@ -946,6 +1005,7 @@ int launch_draw(const csa_instance *I, int32_t k, uint64_t seed, uint64_t panel_
     A.sel0 = I->d_sel0;
     A.rem0 = I->d_rem0;
     A.present0 = I->d_present0;
+    A.pmask = I->d_pmask;
     A.n = I->n;
     A.F = I->F;
     A.W = I->W;
@@ -966,7 +1026,8 @@ int launch_draw(const csa_instance *I, int32_t k, uint64_t seed, uint64_t panel_
     A.rem_out = d_rem_out;
     A.present_out = d_present_out;
     const int groups_wg = kDrawThreads / cfg.G;
-    const size_t lds = draw_lds_bytes(cfg.G, cfg.FPL, cfg.WPL, I->W, k, groups_wg);
+    const size_t lds = cfg.batch ? batch_lds_bytes(cfg.G, cfg.FPL, cfg.WPL, I->n, I->W, k, groups_wg)
+                                 : draw_lds_bytes(cfg.G, cfg.FPL, cfg.WPL, I->W, k, groups_wg);
     if (lds > 160 * 1024) return fail(CSA_E_UNSUPPORTED, "draw kernel needs %zu B of LDS", lds);
     int per_cu = 0, cus = 0;
     HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, cfg.fn, kDrawThreads, lds));
@@ -977,6 +1038,11 @@ int launch_draw(const csa_instance *I, int32_t k, uint64_t seed, uint64_t panel_
     void *args[] = {&A};
     HIPCHK(hipLaunchKernel(cfg.fn, dim3(grid), dim3(kDrawThreads), args, lds, stream));
     HIPCHK(hipGetLastError());
+    if (cfg.batch && d_hashes) {  // the batch kernel leaves hashing to a streaming pass
+        hipLaunchKernelGGL(panel_hash_kernel, dim3((unsigned)((n_panels * 4 + 255) / 256)), dim3(256), 0, stream,
+                           d_panels, n_panels, I->W, d_hashes);
+        HIPCHK(hipGetLastError());
+    }
     return CSA_OK;
 }
 
@@ -1045,6 +1111,7 @@ int csa_instance_create(int32_t n, int32_t C, int32_t F, const int32_t *person_f
         }
     for (int f = 0; f < F; ++f) {
         I->max_abs = std::max(I->max_abs, std::abs(fmin[f]));
+        if (fmax[f] == 0 && fmin[f] != 0) I->zero_max_min = true;
         if (feat_cat[f] < 0 || feat_cat[f] >= C) {
             delete I;
             return fail(CSA_E_INVALID, "feature %d has category %d outside [0,%d)", f, feat_cat[f], C);
@@ -1070,10 +1137,13 @@ int csa_instance_create(int32_t n, int32_t C, int32_t F, const int32_t *person_f
     int rc = CSA_OK;
     if ((rc = dalloc(&I->d_featmask, I->featmask.size())) || (rc = dalloc(&I->d_fmin, F)) ||
         (rc = dalloc(&I->d_fmax, F)) || (rc = dalloc(&I->d_sel0, F)) || (rc = dalloc(&I->d_rem0, F)) ||
-        (rc = dalloc(&I->d_present0, I->W))) {
+        (rc = dalloc(&I->d_present0, I->W)) || (F <= 32 && (rc = dalloc(&I->d_pmask, n)))) {
         csa_instance_destroy(I);
         return rc;
     }
+    std::vector<uint32_t> pmask(F <= 32 ? n : 0, 0u);
+    for (int p = 0; p < (int)pmask.size(); ++p)
+        for (int c = 0; c < C; ++c) pmask[p] |= 1u << person_feat[(size_t)p * C + c];
     hipError_t e = hipSuccess;
     e = e ? e : hipMemcpy(I->d_featmask, I->featmask.data(), I->featmask.size() * 8, hipMemcpyHostToDevice);
     e = e ? e : hipMemcpy(I->d_fmin, fmin, F * 4, hipMemcpyHostToDevice);
@@ -1081,6 +1151,7 @@ int csa_instance_create(int32_t n, int32_t C, int32_t F, const int32_t *person_f
     e = e ? e : hipMemcpy(I->d_sel0, zeros.data(), F * 4, hipMemcpyHostToDevice);
     e = e ? e : hipMemcpy(I->d_rem0, I->pool.data(), F * 4, hipMemcpyHostToDevice);
     if (I->W) e = e ? e : hipMemcpy(I->d_present0, present.data(), I->W * 8, hipMemcpyHostToDevice);
+    if (!pmask.empty()) e = e ? e : hipMemcpy(I->d_pmask, pmask.data(), pmask.size() * 4, hipMemcpyHostToDevice);
     if (e != hipSuccess) {
         csa_instance_destroy(I);
         return fail(CSA_E_HIP, "instance upload: %s", hipGetErrorString(e));
@@ -1098,6 +1169,7 @@ void csa_instance_destroy(csa_instance *I) {
     if (I->d_sel0) (void)hipFree(I->d_sel0);
     if (I->d_rem0) (void)hipFree(I->d_rem0);
     if (I->d_present0) (void)hipFree(I->d_present0);
+    if (I->d_pmask) (void)hipFree(I->d_pmask);
     delete I;
 }
 
