@@ -1025,18 +1025,19 @@ int launch_draw(const csa_instance *I, int32_t k, uint64_t seed, uint64_t panel_
     A.sel_out = d_sel_out;
     A.rem_out = d_rem_out;
     A.present_out = d_present_out;
-    const int groups_wg = kDrawThreads / cfg.G;
+    const int threads = cfg.batch ? kBatchThreads : kDrawThreads;
+    const int groups_wg = threads / cfg.G;
     const size_t lds = cfg.batch ? batch_lds_bytes(cfg.G, cfg.FPL, cfg.WPL, I->n, I->W, k, groups_wg)
                                  : draw_lds_bytes(cfg.G, cfg.FPL, cfg.WPL, I->W, k, groups_wg);
     if (lds > 160 * 1024) return fail(CSA_E_UNSUPPORTED, "draw kernel needs %zu B of LDS", lds);
     int per_cu = 0, cus = 0;
-    HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, cfg.fn, kDrawThreads, lds));
+    HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, cfg.fn, threads, lds));
     HIPCHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, I->device));
     const uint64_t want = (n_panels + groups_wg - 1) / groups_wg;
     const uint64_t cap = (uint64_t)std::max(per_cu, 1) * (uint64_t)std::max(cus, 1);
     const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min(want, cap));
     void *args[] = {&A};
-    HIPCHK(hipLaunchKernel(cfg.fn, dim3(grid), dim3(kDrawThreads), args, lds, stream));
+    HIPCHK(hipLaunchKernel(cfg.fn, dim3(grid), dim3(threads), args, lds, stream));
     HIPCHK(hipGetLastError());
     if (cfg.batch && d_hashes) {  // the batch kernel leaves hashing to a streaming pass
         hipLaunchKernelGGL(panel_hash_kernel, dim3((unsigned)((n_panels * 4 + 255) / 256)), dim3(256), 0, stream,

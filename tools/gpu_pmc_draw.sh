@@ -1,9 +1,9 @@
 #!/bin/bash
 # PMC passes (SQ instruction mix / stalls / LDS) over the bench for each CSA_DRAW_GROUP.
 set -u
-ROOT=${GRAFT_REPO_ROOT:-$(pwd)}; TAG=${1:-pd}; shift || true
+ROOT=${GRAFT_REPO_ROOT:-$(pwd)}; TAG=${1:-pd}; shift || true; GL=${1:-8 4}; shift || true
 export TMPDIR=/tmp; cd /tmp
-for g in ${GROUPS_TO_TRY:-8 4}; do
+for g in $GL; do
   OUT=$ROOT/gpurun_out/prof_${TAG}_g$g; mkdir -p "$OUT"
   for pass in "trace:--kernel-trace --stats" \
               "pmc_sq1:--pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU" \
