@@ -140,7 +140,8 @@ def main():
                              pair_engine=engine_id)
     table = Dd.HashTable(S * world, dev) if world > 1 else None
 
-    stages = ["draw", "xt_count", "pairs", "unique", "exchange"]
+    draw_name = pipe.draw_kernel_name()   # the kernel csa_draw_async launches (matches rocprofv3 names)
+    stages = ["draw", "hash", "xt_count", "pairs", "unique", "exchange"]
     ev_log = []
 
     def step(i, record):
@@ -152,21 +153,24 @@ def main():
         pipe.draw(args.seed, begin, S)
         if evs:
             evs[1].record(stream)
-        pipe.transpose_count(S)
+        pipe.hash(S)
         if evs:
             evs[2].record(stream)
+        pipe.transpose_count(S)
+        if evs:
+            evs[3].record(stream)
         if want_pairs:
             pipe.pair_counts(S)
         if evs:
-            evs[3].record(stream)
+            evs[4].record(stream)
         if world == 1:
             pipe.unique_count(S)
         if evs:
-            evs[4].record(stream)
+            evs[5].record(stream)
         if world > 1:
             Dd.combine(pipe.counts, pipe.pairs, pipe.hashes[: 2 * S], table=table, stream=stream)
         if evs:
-            evs[5].record(stream)
+            evs[6].record(stream)
             ev_log.append(evs)
 
     for i in range(args.warmup):
@@ -198,7 +202,8 @@ def main():
     n, W = enc.n, enc.W
     npad = pipe.npad
     nblk = (S + 63) // 64
-    draw_bytes = S * (8 * W + 16)                         # packed panel + 128-bit hash per panel
+    draw_bytes = S * 8 * W                                # packed panel per panel (written once)
+    hash_bytes = S * (8 * W + 16)                         # read the panel, write its 128-bit hash
     xt_bytes = S * 8 * W + nblk * npad * 8 + n * 8        # read panels, write transposed bits + counts
     pair_ops = S * n * (n + 1)                            # triangle form of 2*S*n^2
     uniq_bytes = S * (16 + 8 * 2)                         # hashes + table slot traffic (approx.)
@@ -207,8 +212,11 @@ def main():
         return b / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
 
     kernels = {
-        "draw": {"ms": stage_ms["draw"], "panels_per_s": S / (stage_ms["draw"] * 1e-3) if stage_ms["draw"] else 0,
+        "draw": {"kernel": draw_name, "ms": stage_ms["draw"],
+                 "panels_per_s": S / (stage_ms["draw"] * 1e-3) if stage_ms["draw"] else 0,
                  "bound": "issue (VALU/LDS latency)", "hbm_GBps": gbs(draw_bytes, stage_ms["draw"])},
+        "hash": {"kernel": "panel_hash_kernel", "ms": stage_ms["hash"], "hbm_GBps": gbs(hash_bytes, stage_ms["hash"]),
+                 "frac": gbs(hash_bytes, stage_ms["hash"]) * 1e9 / HBM_PEAK},
         "xt_count": {"ms": stage_ms["xt_count"], "hbm_GBps": gbs(xt_bytes, stage_ms["xt_count"]),
                      "frac": gbs(xt_bytes, stage_ms["xt_count"]) * 1e9 / HBM_PEAK},
         "unique": {"ms": stage_ms["unique"], "hbm_GBps": gbs(uniq_bytes, stage_ms["unique"])},
@@ -223,24 +231,29 @@ def main():
                                          "ms includes the partial-block reduce kernel"}
     if world > 1:
         kernels["exchange"] = {"ms": stage_ms["exchange"]}
-    dominant = max(("draw", "xt_count", "pairs", "unique"), key=lambda s: stage_ms[s])
+    dominant = max(("draw", "hash", "xt_count", "pairs", "unique"), key=lambda s: stage_ms[s])
     pmc = load_pmc_traffic(args.config)
     if dominant == "pairs":
         ach = pair_ops / (stage_ms["pairs"] * 1e-3) / 1e12
         roof = {"kernel": "pair_mfma_kernel", "bound": "mfma", "achieved": ach, "peak": engine_peak / 1e12,
                 "unit": "TFLOP/s", "frac": ach * 1e12 / engine_peak, "traffic": None}
     else:
-        name = {"draw": "draw_kernel", "xt_count": "xt_count_kernel", "unique": "unique_kernel"}[dominant]
-        b = {"draw": draw_bytes, "xt_count": xt_bytes, "unique": uniq_bytes}[dominant]
+        name = {"draw": draw_name, "hash": "panel_hash_kernel", "xt_count": "xt_count_kernel",
+                "unique": "unique_kernel"}[dominant]
+        b = {"draw": draw_bytes, "hash": hash_bytes, "xt_count": xt_bytes, "unique": uniq_bytes}[dominant]
         ach = gbs(b, stage_ms[dominant])
         traffic = None
-        if pmc and pmc.get("kernel") == name and pmc.get("panels") == S:
-            traffic = pmc.get("hbm_bytes_per_launch")
-        if pmc and name == "draw_kernel" and pmc.get("draw_issue"):
-            kernels["draw"]["pmc_issue"] = pmc["draw_issue"]     # committed rocprofv3 --pmc pass
+        pk = (pmc or {}).get("per_kernel", {}).get(name)
+        if pk and pmc.get("panels") == S:
+            traffic = pk.get("hbm_bytes_per_launch")     # committed rocprofv3 --pmc FETCH/WRITE passes
         roof = {"kernel": name, "bound": "hbm", "achieved": ach, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
-                "frac": ach * 1e9 / HBM_PEAK, "traffic": traffic,
-                "note": "draw_kernel is VALU/LDS issue-bound; its HBM bytes are the panel+hash writes"}
+                "frac": ach * 1e9 / HBM_PEAK, "traffic": traffic}
+        if dominant == "draw":
+            roof["note"] = ("the draw kernel has no HBM or MFMA roof: it is VALU/LDS issue-bound; 'achieved' is "
+                            "its packed-panel writes; issue_frac is the VALU issue-slot fraction from rocprofv3 PMC")
+            if pmc and pmc.get("draw_issue") and pmc.get("draw_kernel") == draw_name:
+                kernels["draw"]["pmc_issue"] = pmc["draw_issue"]
+                roof["issue_frac"] = pmc["draw_issue"].get("valu_issue_frac")
 
     total = S * world * args.steps
     result = {

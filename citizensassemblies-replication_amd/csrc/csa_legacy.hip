@@ -1229,6 +1229,28 @@ int csa_draw_async(const csa_instance *I, int32_t k, uint64_t seed, uint64_t pan
                        d_picks, d_status, nullptr, nullptr, nullptr, (hipStream_t)stream);
 }
 
+int csa_panel_hash_async(const uint64_t *d_panels, uint64_t n_panels, int32_t W, uint64_t *d_hashes,
+                         void *stream) {
+    if (W <= 0 || !d_panels || !d_hashes) return fail(CSA_E_INVALID, "panel hash: bad arguments");
+    if (n_panels == 0) return CSA_OK;
+    hipLaunchKernelGGL(panel_hash_kernel, dim3((unsigned)((n_panels * 4 + 255) / 256)), dim3(256), 0,
+                       (hipStream_t)stream, d_panels, n_panels, W, d_hashes);
+    HIPCHK(hipGetLastError());
+    return CSA_OK;
+}
+
+int csa_draw_kernel_name(const csa_instance *I, int32_t k, char *buf, uint64_t len) {
+    if (!I || !buf || len == 0) return fail(CSA_E_INVALID, "draw kernel name: bad arguments");
+    int rc = check_k(I, k);
+    if (rc) return rc;
+    DrawConfig cfg;
+    rc = pick_draw_config(I, false, cfg);
+    if (rc) return rc;
+    snprintf(buf, (size_t)len, "%s<%d, %d, %d%s>", cfg.batch ? "draw_batch_kernel" : "draw_kernel", cfg.G, cfg.FPL,
+             cfg.WPL, cfg.batch ? "" : ", false");
+    return CSA_OK;
+}
+
 int32_t csa_xt_pad(int32_t n) { return ((n + kPairBlock - 1) / kPairBlock) * kPairBlock; }
 
 int csa_transpose_count_async(const uint64_t *d_panels, uint64_t n_panels, int32_t n, uint64_t *d_xt,

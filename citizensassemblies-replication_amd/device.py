@@ -4,7 +4,8 @@ PyTorch only provides device memory, the stream and (in distributed.py) the
 RCCL collectives; every kernel is the hand-written HIP in csrc/.  One
 ``run`` = one pass of analysis.py:162-191 over a shard of panels:
 
-    draw_kernel        panels [panel_begin, panel_begin+S) -> packed bitmasks + 128-bit hashes
+    draw_(batch_)kernel  panels [panel_begin, panel_begin+S) -> packed bitmasks
+    panel_hash_kernel  bitmasks -> 128-bit panel hashes                    (if want_unique)
     xt_count_kernel    bitmasks -> transposed panel-indicator bits + per-person counts (+=)
     pair_mfma_kernel   transposed bits -> int32 partial blocks of X^T X on fp4 (default) or
     pair_reduce_kernel   int8 MFMA -> pair counts (+=)                  (if want_pairs)
@@ -72,9 +73,18 @@ class DevicePipeline:
     def draw(self, seed, panel_begin, S, max_attempts=0):
         assert S <= self.max_panels
         N.check(N.lib().csa_draw_async(self.enc.handle, self.k, int(seed) & 0xFFFFFFFFFFFFFFFF, int(panel_begin),
-                                       int(S), max_attempts, N.ptr(self.panels), N.ptr(self.hashes),
+                                       int(S), max_attempts, N.ptr(self.panels), None,
                                        N.ptr(self.attempts), None, N.ptr(self.status),
                                        _stream_ptr(self.stream)))
+
+    def hash(self, S):
+        N.check(N.lib().csa_panel_hash_async(N.ptr(self.panels), int(S), self.enc.W, N.ptr(self.hashes),
+                                             _stream_ptr(self.stream)))
+
+    def draw_kernel_name(self):
+        buf = ctypes.create_string_buffer(128)
+        N.check(N.lib().csa_draw_kernel_name(self.enc.handle, self.k, buf, 128))
+        return buf.value.decode()
 
     def transpose_count(self, S):
         N.check(N.lib().csa_transpose_count_async(N.ptr(self.panels), int(S), self.enc.n,
@@ -98,6 +108,8 @@ class DevicePipeline:
     def run(self, seed, panel_begin, S, max_attempts=0):
         """Enqueue the whole pass; results accumulate into counts / pairs / unique."""
         self.draw(seed, panel_begin, S, max_attempts)
+        if self.want_unique:
+            self.hash(S)
         self.transpose_count(S)
         if self.want_pairs:
             self.pair_counts(S)

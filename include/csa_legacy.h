@@ -123,6 +123,16 @@ int csa_draw_async(const csa_instance *inst, int32_t k, uint64_t seed, uint64_t 
                    uint64_t *d_hashes, uint32_t *d_attempts, int32_t *d_picks,
                    uint32_t *d_status, void *stream);
 
+/* 128-bit panel hashes (2*n_panels uint64) of packed panels (n_panels*W), the
+ * key of the distinct-panel count (replaces hashing the sorted tuples of
+ * analysis.py:171,186); identical to the hashes csa_draw_async writes. */
+int csa_panel_hash_async(const uint64_t *d_panels, uint64_t n_panels, int32_t W, uint64_t *d_hashes,
+                         void *stream);
+
+/* Name of the draw kernel csa_draw_async launches for this instance and k
+ * (e.g. "draw_batch_kernel<4, 8, 8>"), for matching profiler output. */
+int csa_draw_kernel_name(const csa_instance *inst, int32_t k, char *buf, uint64_t len);
+
 /* Bit-transpose + per-person count.  Panels (n_panels*W) -> d_xt, the
  * panel-indicator matrix transposed and packed: d_xt[b * n_pad + p] holds
  * bits of agent p for panels 64b..64b+63; n_pad = csa_xt_pad(n), blocks

@@ -68,6 +68,7 @@ def main():
         out["per_kernel"][k] = e
     if draw_name:
         out["kernel"] = draw_name
+        out["draw_kernel"] = draw_name
         out["hbm_bytes_per_launch"] = out["per_kernel"][draw_name].get("hbm_bytes_per_launch")
     s = json.dumps(out, indent=1)
     print(s)
