@@ -3,7 +3,7 @@
 set -u
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}; OUT=$ROOT/gpurun_out; mkdir -p "$OUT"; cd "$ROOT"
 TAG=${1:-dc}; shift || true; GL=${1:-16 8 4}; shift || true
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -k "parity or pairs" > "$OUT/pytest_$TAG.log" 2>&1
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -k "parity or pairs or draw" > "$OUT/pytest_$TAG.log" 2>&1
 rc=$?; tail -8 "$OUT/pytest_$TAG.log"; echo "[pytest] rc=$rc"
 [ $rc -eq 0 ] || exit $rc
 for g in $GL; do
