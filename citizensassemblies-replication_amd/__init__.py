@@ -7,11 +7,14 @@ reference's legacy.py / analysis.py LEGACY functions:
 
     read_instance, Instance, PairHistogram, SelectionError, check_min_cats,
     find_random_sample_legacy, legacy_find, legacy_probabilities, seed
+
+plus xmin._get_panel_not_in_portfolio_if_possible (XMIN's LEGACY caller,
+xmin.py:464-474) on the device.
 """
 from .instance import Instance, read_instance, encode  # noqa: F401
 from .legacy import SelectionError, check_min_cats, find_random_sample_legacy, seed  # noqa: F401
 from .analysis import PairHistogram, PanelSet, legacy_find, legacy_find_batch, legacy_probabilities  # noqa: F401
-from . import _native  # noqa: F401
+from . import _native, xmin  # noqa: F401
 
 __all__ = ["Instance", "read_instance", "encode", "SelectionError", "check_min_cats",
            "find_random_sample_legacy", "seed", "PairHistogram", "PanelSet", "legacy_find",

@@ -47,6 +47,7 @@ SIGNATURES = {
     "csa_legacy_sample": (ctypes.c_int, [_P, _I32, _U64, _U64, _U64, _U32, _U32, _P, _P, _P, _P, _P]),
     "csa_legacy_find": (ctypes.c_int, [_P, _I32, _U64, _U64, _U64, _U32, _P, _P]),
     "csa_legacy_attempt": (ctypes.c_int, [_P, _I32, _U64, _U64, _U32, _P, _P, _P, _P, _P]),
+    "csa_first_panel_not_in": (ctypes.c_int, [_P, _I32, _U64, _U64, _U64, _U32, _P, _U64, _U64, _P, _P]),
     "csa_draw_async": (ctypes.c_int, [_P, _I32, _U64, _U64, _U64, _U32, _P, _P, _P, _P, _P, _P]),
     "csa_panel_hash_async": (ctypes.c_int, [_P, _U64, _I32, _P, _P]),
     "csa_draw_kernel_name": (ctypes.c_int, [_P, _I32, ctypes.c_char_p, _U64]),

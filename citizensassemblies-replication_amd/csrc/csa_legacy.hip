@@ -851,6 +851,31 @@ __global__ void unique_kernel(const uint64_t *__restrict__ hashes, const uint64_
     if ((threadIdx.x & 63) == 0 && b) atomicAdd(unique, (unsigned long long)__popcll(b));
 }
 
+// Portfolio membership of drawn panels (xmin.py:468-469: `panel not in portfolio`): probe the
+// portfolio table built by unique_kernel (slots hold portfolio index + 1) with each drawn panel's
+// hash and compare full bitmasks on a hash match; the lowest non-member index wins (atomicMin).
+__global__ void member_scan_kernel(const uint64_t *__restrict__ hashes, const uint64_t *__restrict__ panels,
+                                   uint64_t S, int W, const unsigned long long *__restrict__ table, uint64_t mask,
+                                   const uint64_t *__restrict__ port_hashes, const uint64_t *__restrict__ port_panels,
+                                   unsigned long long *__restrict__ first) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= S) return;
+    const uint64_t h1 = hashes[2 * i], h2 = hashes[2 * i + 1];
+    uint64_t slot = (h1 ^ (h2 >> 29)) & mask;
+    for (uint64_t probe = 0; probe <= mask; ++probe) {
+        const unsigned long long v = table[slot];
+        if (v == 0ull) break;  // empty slot: not a member
+        const uint64_t j = v - 1;
+        if (port_hashes[2 * j] == h1 && port_hashes[2 * j + 1] == h2) {
+            bool same = true;
+            for (int w = 0; w < W && same; ++w) same = panels[i * W + w] == port_panels[j * W + w];
+            if (same) return;  // member
+        }
+        slot = (slot + 1) & mask;
+    }
+    atomicMin(first, (unsigned long long)i);
+}
+
 }  // namespace
 
 // ==========================================================================================
@@ -1443,6 +1468,79 @@ int csa_legacy_sample(csa_instance *I, int32_t k, uint64_t seed, uint64_t panel_
     if (want_unique) HIPCHK(hipMemcpyAsync(unique_out, uniq.p, 8, hipMemcpyDeviceToHost, st));
     if (attempts_out) HIPCHK(hipMemcpyAsync(attempts_out, attempts.p, n_panels * 4, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
+    return CSA_OK;
+}
+
+int csa_first_panel_not_in(csa_instance *I, int32_t k, uint64_t seed, uint64_t panel_begin, uint64_t n_panels,
+                           uint32_t max_attempts, const uint64_t *portfolio, uint64_t m, uint64_t chunk,
+                           int64_t *index_out, uint64_t *panel_out) {
+    if (!I || !index_out || !panel_out || (m && !portfolio)) return fail(CSA_E_INVALID, "first_panel_not_in: bad arguments");
+    *index_out = -1;
+    if (n_panels == 0) return CSA_OK;
+    ScopedDevice sd(I->device);
+    const int W = I->W;
+    if (chunk == 0) chunk = 256;
+    hipStream_t st = nullptr;
+    HIPCHK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    struct StreamGuard {
+        hipStream_t s;
+        ~StreamGuard() { (void)hipStreamDestroy(s); }
+    } sg{st};
+    const uint64_t cap = std::min(n_panels, std::max<uint64_t>(chunk, 1) << 12);  // largest chunk
+    const uint64_t slots = pow2_at_least(std::max<uint64_t>(2 * m, 64));
+    DevBuf<uint64_t> pport, phash, table, cnt, panels, hashes, first;
+    DevBuf<uint32_t> status;
+    int rc;
+    if ((rc = dalloc(&pport.p, std::max<uint64_t>(m, 1) * W)) || (rc = dalloc(&phash.p, 2 * std::max<uint64_t>(m, 1))) ||
+        (rc = dalloc(&table.p, slots)) || (rc = dalloc(&cnt.p, 1)) || (rc = dalloc(&panels.p, cap * W)) ||
+        (rc = dalloc(&hashes.p, 2 * cap)) || (rc = dalloc(&first.p, 1)) || (rc = dalloc(&status.p, 4)))
+        return rc;
+    HIPCHK(hipMemsetAsync(table.p, 0, slots * 8, st));
+    if (m) {  // portfolio table: panel_hash_kernel + unique_kernel insertion (exact)
+        HIPCHK(hipMemcpyAsync(pport.p, portfolio, m * W * 8, hipMemcpyHostToDevice, st));
+        if ((rc = csa_panel_hash_async(pport.p, m, W, phash.p, st))) return rc;
+        HIPCHK(hipMemsetAsync(cnt.p, 0, 8, st));
+        if ((rc = csa_unique_async(phash.p, pport.p, m, W, table.p, slots, cnt.p, st))) return rc;
+    }
+    // chunks of growing size: the expected first non-member is near the start
+    uint64_t done = 0, len = std::min(chunk, n_panels);
+    while (done < n_panels) {
+        len = std::min(len, n_panels - done);
+        HIPCHK(hipMemsetAsync(status.p, 0, 16, st));
+        HIPCHK(hipMemsetAsync(first.p, 0xFF, 8, st));
+        if ((rc = launch_draw(I, k, seed, panel_begin + done, len, max_attempts, 0, 0, panels.p, nullptr, nullptr,
+                              nullptr, status.p, nullptr, nullptr, nullptr, st)))
+            return rc;
+        if ((rc = csa_panel_hash_async(panels.p, len, W, hashes.p, st))) return rc;
+        hipLaunchKernelGGL(member_scan_kernel, dim3((unsigned)((len + 255) / 256)), dim3(256), 0, st, hashes.p,
+                           panels.p, len, W, reinterpret_cast<const unsigned long long *>(table.p), slots - 1,
+                           phash.p, pport.p, reinterpret_cast<unsigned long long *>(first.p));
+        HIPCHK(hipGetLastError());
+        uint32_t hs[4];
+        if ((rc = read_status(status.p, st, hs))) return rc;
+        if (hs[0] != 0u) {
+            // a draw error (KeyError / attempt limit) at panel e: the reference meets it only if
+            // every panel before e is a member, so re-scan the panels before e first (the error
+            // stops other groups, leaving later panels of this chunk undrawn)
+            const uint64_t e = (uint64_t)hs[1] | ((uint64_t)hs[2] << 32), start = panel_begin + done;
+            if (e > start && e < start + len) {
+                len = e - start;
+                continue;
+            }
+            return csa_status_decode(hs);
+        }
+        uint64_t f = 0;
+        HIPCHK(hipMemcpyAsync(&f, first.p, 8, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        if (f != ~0ull) {
+            HIPCHK(hipMemcpyAsync(panel_out, panels.p + f * W, (size_t)W * 8, hipMemcpyDeviceToHost, st));
+            HIPCHK(hipStreamSynchronize(st));
+            *index_out = (int64_t)(done + f);
+            return CSA_OK;
+        }
+        done += len;
+        len = std::min<uint64_t>(len * 2, cap);
+    }
     return CSA_OK;
 }
 

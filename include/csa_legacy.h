@@ -108,6 +108,17 @@ int csa_legacy_attempt(csa_instance *inst, int32_t k, uint64_t seed, uint64_t pa
                        uint32_t attempt, int32_t *picks_out, int32_t *n_picks, int32_t *sel_out,
                        int32_t *rem_out, uint64_t *present_out);
 
+/* XMIN's LEGACY caller (_get_panel_not_in_portfolio_if_possible, xmin.py:464-474):
+ * draw panels panel_begin, panel_begin+1, ... (at most n_panels; chunks of `chunk`
+ * panels, doubling) and stop at the first one that is not in the portfolio (m packed
+ * panels, host memory, m*W uint64; exact bitmask comparison behind a device hash
+ * table).  *index_out = its offset from panel_begin (-1: all n_panels are members),
+ * panel_out (W uint64) = that panel.  A draw error (KeyError / attempt limit) is
+ * returned only if every panel before it is a member, as in the reference loop. */
+int csa_first_panel_not_in(csa_instance *inst, int32_t k, uint64_t seed, uint64_t panel_begin,
+                           uint64_t n_panels, uint32_t max_attempts, const uint64_t *portfolio,
+                           uint64_t m, uint64_t chunk, int64_t *index_out, uint64_t *panel_out);
+
 /* ---- stream-ordered device API ---------------------------------------------
  * All buffers are device pointers on the instance's device; `stream` is a
  * hipStream_t (NULL = default stream).  Nothing synchronises; errors inside

@@ -108,3 +108,17 @@ def test_check_min_cats():
     assert not ok and msg == ["Failed to get minimum in category: m"]
     cats["g"]["m"]["selected"] = 2
     assert L.check_min_cats(cats) == (True, [])
+
+
+def test_pack_portfolio_roundtrip():
+    """xmin.pack_portfolio: agent-id panels -> bitmask rows (unknown agents drop the panel)."""
+    P = pkg()
+    X = pkg("xmin")
+    inst = P.read_instance(*inst_paths("example_small_20"), 20)
+    enc = P.encode(inst.categories, inst.agents)
+    ids = list(inst.agents)
+    panels = [frozenset(ids[3:23]), frozenset(ids[150:170]), frozenset(ids[:19] + ["nobody"])]
+    rows = X.pack_portfolio(enc, panels)
+    assert rows.shape == (2, enc.W)
+    for r, pnl in zip(rows, panels[:2]):
+        assert frozenset(enc.agent_ids[p] for p in P.instance.unpack_panel(r, enc.n)) == pnl
