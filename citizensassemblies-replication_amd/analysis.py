@@ -18,7 +18,7 @@ from typing import Dict, List, Tuple
 import numpy as np
 
 from . import _native as N
-from .instance import Instance, read_instance, encode, unpack_panel  # noqa: F401
+from .instance import Instance, read_instance, encode, encode_cached, unpack_panel  # noqa: F401
 from .legacy import STREAM, seed, SelectionError, check_min_cats  # noqa: F401
 
 ProbAllocation = Dict
@@ -42,6 +42,7 @@ class PairHistogram:
             assert self._m.shape == (n, n)
         else:
             self._m = np.zeros((n, n), np.int64)
+        self._counts = self._S = None   # integer pair counts and S when built by finish()
         if uniform_distribution:
             npairs = n * (n - 1) // 2
             self._m = np.full((n, n), 1 / npairs if npairs else 0.0, np.float64)
@@ -60,14 +61,17 @@ class PairHistogram:
 
     def __setitem__(self, key, value):
         i, j = self._key(key)
+        self._counts = self._S = None
         if isinstance(value, float) and self._m.dtype.kind != "f":
             self._m = self._m.astype(np.float64)
         self._m[i, j] = value
 
     def turn_into_probabilities_by_dividing_all_elements_by_given_number(self, num):
         self._m = self._m / num
+        self._counts = self._S = None
 
     def add_portfolio_of_panels_to_histogram(self, portfolio, probabilities):
+        self._counts = self._S = None
         for panel, pob in zip(portfolio, probabilities):
             idx = np.asarray(sorted(panel), np.int64)
             if isinstance(pob, float) and self._m.dtype.kind != "f":
@@ -92,6 +96,7 @@ class PairHistogram:
 
     def __setstate__(self, st):
         self.n, self._m = st["n"], st["m"]
+        self._counts = self._S = None
 
 
 class PanelSet:
@@ -132,7 +137,7 @@ class PanelSet:
 
 def legacy_find(feature_info, agents, k) -> List:
     """analysis.py:141-159: one accepted panel, pick order, restarts on the device."""
-    enc = encode(feature_info, agents)
+    enc = encode_cached(feature_info, agents)
     k = int(k)
     picks = np.full(max(k, 1), -1, np.int32)
     first = STREAM.take_panels(1)
@@ -142,7 +147,7 @@ def legacy_find(feature_info, agents, k) -> List:
 
 def legacy_find_batch(feature_info, agents, k, count, max_attempts=0):
     """``count`` consecutive legacy_find calls in one launch (XMIN's caller, xmin.py:464-474)."""
-    enc = encode(feature_info, agents)
+    enc = encode_cached(feature_info, agents)
     k = int(k)
     picks = np.full((int(count), max(k, 1)), -1, np.int32)
     first = STREAM.take_panels(count)
@@ -209,5 +214,6 @@ def finish(instance, enc, raw, S):
     alloc = {aid: int(raw.counts[p]) / S for p, aid in enumerate(enc.agent_ids)}
     hist = PairHistogram(len(instance.agents), counts=raw.pairs)
     hist.turn_into_probabilities_by_dividing_all_elements_by_given_number(S)
+    hist._counts, hist._S = raw.pairs, S      # integer counts for stats.sorted_pair_probabilities
     panels = PanelSet(raw.unique, raw.panels, enc.n, enc.agent_ids)
     return alloc, panels, hist

@@ -876,6 +876,53 @@ __global__ void member_scan_kernel(const uint64_t *__restrict__ hashes, const ui
     atomicMin(first, (unsigned long long)i);
 }
 
+// Histogram of the pair counts i < j (the values plot_pair_probability_distribution_per_algorithm
+// sorts, analysis.py:339-342): one workgroup per row i, coalesced reads of pairs[i][i+1..n),
+// one 64-bit atomic per entry into hist[value] (value < n_bins is guaranteed by the caller:
+// n_bins > max per-person count >= every pair count).  Values >= n_bins are counted in *overflow.
+__global__ __launch_bounds__(256) void pair_histogram_kernel(const int64_t *__restrict__ pairs, int n,
+                                                             unsigned long long *__restrict__ hist, uint64_t n_bins,
+                                                             unsigned long long *__restrict__ overflow) {
+    const int i = blockIdx.x;
+    const int64_t *row = pairs + (size_t)i * n;
+    for (int j = i + 1 + (int)threadIdx.x; j < n; j += blockDim.x) {
+        const uint64_t v = (uint64_t)row[j];
+        if (v < n_bins)
+            atomicAdd(hist + v, 1ull);
+        else
+            atomicAdd(overflow, 1ull);
+    }
+}
+
+// Small-range variant (n_bins <= kHistLdsBins): per-workgroup LDS histogram over a stride of
+// rows (u32 LDS atomics), flushed with one global atomic per non-zero bin -- few distinct values
+// (n = 8192, S = 2e4: ~700 bins for 33.5 M pairs) would otherwise serialise on global atomics.
+constexpr int kHistLdsBins = 16384;
+__global__ __launch_bounds__(256) void pair_histogram_lds_kernel(const int64_t *__restrict__ pairs, int n,
+                                                                 unsigned long long *__restrict__ hist,
+                                                                 uint64_t n_bins,
+                                                                 unsigned long long *__restrict__ overflow) {
+    __shared__ uint32_t h[kHistLdsBins];
+    __shared__ uint32_t over_s;
+    for (int b = threadIdx.x; b < (int)n_bins; b += blockDim.x) h[b] = 0;
+    if (threadIdx.x == 0) over_s = 0;
+    __syncthreads();
+    for (int i = blockIdx.x; i < n - 1; i += gridDim.x) {
+        const int64_t *row = pairs + (size_t)i * n;
+        for (int j = i + 1 + (int)threadIdx.x; j < n; j += blockDim.x) {
+            const uint64_t v = (uint64_t)row[j];
+            if (v < n_bins)
+                atomicAdd(&h[v], 1u);
+            else
+                atomicAdd(&over_s, 1u);
+        }
+    }
+    __syncthreads();
+    for (int b = threadIdx.x; b < (int)n_bins; b += blockDim.x)
+        if (h[b]) atomicAdd(hist + b, (unsigned long long)h[b]);
+    if (threadIdx.x == 0 && over_s) atomicAdd(overflow, (unsigned long long)over_s);
+}
+
 }  // namespace
 
 // ==========================================================================================
@@ -892,6 +939,11 @@ struct csa_instance {
     uint32_t *d_pmask = nullptr;  // n person feature masks (F <= 32 only)
     int32_t max_abs = 0;  // max |fmin| / |sel0| bound for the cross-multiplication range check
     bool zero_max_min = false;  // some feature has max 0 and min > 0 (draw_batch_kernel excludes it)
+    // grow-only device scratch + a stream for the repeated small host-API calls
+    // (csa_first_panel_not_in: XMIN calls it 5n times)
+    void *scratch[8] = {};
+    size_t scratch_bytes[8] = {};
+    hipStream_t stream = nullptr;
 };
 
 namespace {
@@ -1092,6 +1144,21 @@ struct DevBuf {
     }
 };
 
+// instance scratch slot `slot` with at least `count` elements (grow-only)
+template <typename T>
+int scratch(csa_instance *I, int slot, size_t count, T **out) {
+    const size_t bytes = std::max<size_t>(count, 1) * sizeof(T);
+    if (I->scratch_bytes[slot] < bytes) {
+        if (I->scratch[slot]) HIPCHK(hipFree(I->scratch[slot]));
+        I->scratch[slot] = nullptr;
+        I->scratch_bytes[slot] = 0;
+        HIPCHK(hipMalloc(&I->scratch[slot], bytes));
+        I->scratch_bytes[slot] = bytes;
+    }
+    *out = static_cast<T *>(I->scratch[slot]);
+    return CSA_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -1196,6 +1263,9 @@ void csa_instance_destroy(csa_instance *I) {
     if (I->d_rem0) (void)hipFree(I->d_rem0);
     if (I->d_present0) (void)hipFree(I->d_present0);
     if (I->d_pmask) (void)hipFree(I->d_pmask);
+    for (int i = 0; i < 8; ++i)
+        if (I->scratch[i]) (void)hipFree(I->scratch[i]);
+    if (I->stream) (void)hipStreamDestroy(I->stream);
     delete I;
 }
 
@@ -1225,6 +1295,27 @@ int csa_instance_set_state(csa_instance *I, const int32_t *sel, const int32_t *r
     HIPCHK(hipMemcpy(I->d_sel0, sel ? sel : zeros.data(), I->F * 4, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(I->d_rem0, rem ? rem : I->pool.data(), I->F * 4, hipMemcpyHostToDevice));
     if (I->W) HIPCHK(hipMemcpy(I->d_present0, present ? present : all.data(), I->W * 8, hipMemcpyHostToDevice));
+    return CSA_OK;
+}
+
+int csa_pair_histogram_async(const int64_t *d_pairs, int32_t n, uint64_t *d_hist, uint64_t n_bins,
+                             uint64_t *d_overflow, void *stream) {
+    if (n < 0 || !d_pairs || !d_hist || !d_overflow || n_bins == 0) return fail(CSA_E_INVALID, "pair histogram: bad arguments");
+    HIPCHK(hipMemsetAsync(d_hist, 0, n_bins * 8, (hipStream_t)stream));
+    HIPCHK(hipMemsetAsync(d_overflow, 0, 8, (hipStream_t)stream));
+    if (n < 2) return CSA_OK;
+    if (n_bins <= (uint64_t)kHistLdsBins) {
+        // ~2 workgroups per CU, each over a stride of rows (one LDS histogram flush per workgroup)
+        const unsigned grid = (unsigned)std::min<int>(n - 1, 512);
+        hipLaunchKernelGGL(pair_histogram_lds_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, d_pairs, n,
+                           reinterpret_cast<unsigned long long *>(d_hist), n_bins,
+                           reinterpret_cast<unsigned long long *>(d_overflow));
+    } else {
+        hipLaunchKernelGGL(pair_histogram_kernel, dim3((unsigned)(n - 1)), dim3(256), 0, (hipStream_t)stream, d_pairs,
+                           n, reinterpret_cast<unsigned long long *>(d_hist), n_bins,
+                           reinterpret_cast<unsigned long long *>(d_overflow));
+    }
+    HIPCHK(hipGetLastError());
     return CSA_OK;
 }
 
@@ -1480,44 +1571,42 @@ int csa_first_panel_not_in(csa_instance *I, int32_t k, uint64_t seed, uint64_t p
     ScopedDevice sd(I->device);
     const int W = I->W;
     if (chunk == 0) chunk = 256;
-    hipStream_t st = nullptr;
-    HIPCHK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
-    struct StreamGuard {
-        hipStream_t s;
-        ~StreamGuard() { (void)hipStreamDestroy(s); }
-    } sg{st};
+    if (!I->stream) HIPCHK(hipStreamCreateWithFlags(&I->stream, hipStreamNonBlocking));
+    hipStream_t st = I->stream;
     const uint64_t cap = std::min(n_panels, std::max<uint64_t>(chunk, 1) << 12);  // largest chunk
     const uint64_t slots = pow2_at_least(std::max<uint64_t>(2 * m, 64));
-    DevBuf<uint64_t> pport, phash, table, cnt, panels, hashes, first;
-    DevBuf<uint32_t> status;
+    uint64_t *pport, *phash, *table, *cnt, *panels, *hashes, *first;
+    uint32_t *status;
     int rc;
-    if ((rc = dalloc(&pport.p, std::max<uint64_t>(m, 1) * W)) || (rc = dalloc(&phash.p, 2 * std::max<uint64_t>(m, 1))) ||
-        (rc = dalloc(&table.p, slots)) || (rc = dalloc(&cnt.p, 1)) || (rc = dalloc(&panels.p, cap * W)) ||
-        (rc = dalloc(&hashes.p, 2 * cap)) || (rc = dalloc(&first.p, 1)) || (rc = dalloc(&status.p, 4)))
+    if ((rc = scratch(I, 0, std::max<uint64_t>(m, 1) * W, &pport)) ||
+        (rc = scratch(I, 1, 2 * std::max<uint64_t>(m, 1), &phash)) || (rc = scratch(I, 2, slots, &table)) ||
+        (rc = scratch(I, 3, 2, &cnt)) || (rc = scratch(I, 4, cap * W, &panels)) ||
+        (rc = scratch(I, 5, 2 * cap, &hashes)) || (rc = scratch(I, 6, 1, &first)) ||
+        (rc = scratch(I, 7, 4, &status)))
         return rc;
-    HIPCHK(hipMemsetAsync(table.p, 0, slots * 8, st));
+    HIPCHK(hipMemsetAsync(table, 0, slots * 8, st));
     if (m) {  // portfolio table: panel_hash_kernel + unique_kernel insertion (exact)
-        HIPCHK(hipMemcpyAsync(pport.p, portfolio, m * W * 8, hipMemcpyHostToDevice, st));
-        if ((rc = csa_panel_hash_async(pport.p, m, W, phash.p, st))) return rc;
-        HIPCHK(hipMemsetAsync(cnt.p, 0, 8, st));
-        if ((rc = csa_unique_async(phash.p, pport.p, m, W, table.p, slots, cnt.p, st))) return rc;
+        HIPCHK(hipMemcpyAsync(pport, portfolio, m * W * 8, hipMemcpyHostToDevice, st));
+        if ((rc = csa_panel_hash_async(pport, m, W, phash, st))) return rc;
+        HIPCHK(hipMemsetAsync(cnt, 0, 8, st));
+        if ((rc = csa_unique_async(phash, pport, m, W, table, slots, cnt, st))) return rc;
     }
     // chunks of growing size: the expected first non-member is near the start
     uint64_t done = 0, len = std::min(chunk, n_panels);
     while (done < n_panels) {
         len = std::min(len, n_panels - done);
-        HIPCHK(hipMemsetAsync(status.p, 0, 16, st));
-        HIPCHK(hipMemsetAsync(first.p, 0xFF, 8, st));
-        if ((rc = launch_draw(I, k, seed, panel_begin + done, len, max_attempts, 0, 0, panels.p, nullptr, nullptr,
-                              nullptr, status.p, nullptr, nullptr, nullptr, st)))
+        HIPCHK(hipMemsetAsync(status, 0, 16, st));
+        HIPCHK(hipMemsetAsync(first, 0xFF, 8, st));
+        if ((rc = launch_draw(I, k, seed, panel_begin + done, len, max_attempts, 0, 0, panels, nullptr, nullptr,
+                              nullptr, status, nullptr, nullptr, nullptr, st)))
             return rc;
-        if ((rc = csa_panel_hash_async(panels.p, len, W, hashes.p, st))) return rc;
-        hipLaunchKernelGGL(member_scan_kernel, dim3((unsigned)((len + 255) / 256)), dim3(256), 0, st, hashes.p,
-                           panels.p, len, W, reinterpret_cast<const unsigned long long *>(table.p), slots - 1,
-                           phash.p, pport.p, reinterpret_cast<unsigned long long *>(first.p));
+        if ((rc = csa_panel_hash_async(panels, len, W, hashes, st))) return rc;
+        hipLaunchKernelGGL(member_scan_kernel, dim3((unsigned)((len + 255) / 256)), dim3(256), 0, st, hashes,
+                           panels, len, W, reinterpret_cast<const unsigned long long *>(table), slots - 1,
+                           phash, pport, reinterpret_cast<unsigned long long *>(first));
         HIPCHK(hipGetLastError());
         uint32_t hs[4];
-        if ((rc = read_status(status.p, st, hs))) return rc;
+        if ((rc = read_status(status, st, hs))) return rc;
         if (hs[0] != 0u) {
             // a draw error (KeyError / attempt limit) at panel e: the reference meets it only if
             // every panel before e is a member, so re-scan the panels before e first (the error
@@ -1530,10 +1619,10 @@ int csa_first_panel_not_in(csa_instance *I, int32_t k, uint64_t seed, uint64_t p
             return csa_status_decode(hs);
         }
         uint64_t f = 0;
-        HIPCHK(hipMemcpyAsync(&f, first.p, 8, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipMemcpyAsync(&f, first, 8, hipMemcpyDeviceToHost, st));
         HIPCHK(hipStreamSynchronize(st));
         if (f != ~0ull) {
-            HIPCHK(hipMemcpyAsync(panel_out, panels.p + f * W, (size_t)W * 8, hipMemcpyDeviceToHost, st));
+            HIPCHK(hipMemcpyAsync(panel_out, panels + f * W, (size_t)W * 8, hipMemcpyDeviceToHost, st));
             HIPCHK(hipStreamSynchronize(st));
             *index_out = (int64_t)(done + f);
             return CSA_OK;

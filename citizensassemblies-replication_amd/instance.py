@@ -129,6 +129,32 @@ def encode(categories, agents) -> EncodedInstance:
     return EncodedInstance(categories, agents)
 
 
+_ENC_CACHE = []        # [(categories, agents, fingerprint, EncodedInstance)], most recent last
+_ENC_CACHE_SIZE = 4
+
+
+def _fingerprint(categories, agents):
+    return (tuple((c, f, v["min"], v["max"], v.get("selected", 0), v.get("remaining", 0))
+                  for c in categories for f, v in categories[c].items()), tuple(agents))
+
+
+def encode_cached(categories, agents) -> EncodedInstance:
+    """``encode`` memoised for callers that draw repeatedly from the same dicts (XMIN's
+    3n-fold legacy_find loop, xmin.py:464-474, called 5n times): the entry is keyed by the
+    dict objects themselves (held, so their ids stay unique) and revalidated by the feature
+    quotas / counters and the agent ids.  In-place edits of a person's feature values are
+    not detected -- the reference's callers never make them."""
+    fp = _fingerprint(categories, agents)
+    for i, (c, a, f, enc) in enumerate(_ENC_CACHE):
+        if c is categories and a is agents and f == fp:
+            _ENC_CACHE.append(_ENC_CACHE.pop(i))
+            return enc
+    enc = EncodedInstance(categories, agents)
+    _ENC_CACHE.append((categories, agents, fp, enc))
+    del _ENC_CACHE[:-_ENC_CACHE_SIZE]
+    return enc
+
+
 def unpack_panel(words, n):
     """uint64[W] -> sorted list of bit positions."""
     bits = np.unpackbits(np.ascontiguousarray(words, np.uint64).view(np.uint8), bitorder="little")[:n]

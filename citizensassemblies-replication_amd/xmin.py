@@ -14,27 +14,43 @@ import ctypes
 import numpy as np
 
 from . import _native as N
-from .instance import encode, unpack_panel
+from .instance import encode_cached, unpack_panel
 from .legacy import STREAM
+
+
+_ROW_CACHE = {}      # id(enc) -> (enc, {panel: packed row or None}); XMIN's portfolio grows by one per call
+
+
+def _pack_one(pos, W, panel):
+    row = np.zeros(W, np.uint64)
+    for aid in panel:
+        p = pos.get(aid)
+        if p is None:
+            return None
+        row[p >> 6] |= np.uint64(1) << np.uint64(p & 63)
+    return row
 
 
 def pack_portfolio(enc, portfolio):
     """Portfolio panels (iterables of agent ids) -> uint64[m, W] packed bitmasks.
 
     Panels naming an agent outside the instance can never equal a drawn panel and
-    are left out (membership of drawn panels is unchanged)."""
-    pos = {aid: p for p, aid in enumerate(enc.agent_ids)}
+    are left out (membership of drawn panels is unchanged).  Rows of hashable panels
+    (frozensets, as XMIN's portfolio holds) are memoised per encoding."""
+    ent = _ROW_CACHE.get(id(enc))
+    if ent is None or ent[0] is not enc:
+        _ROW_CACHE.clear()
+        ent = _ROW_CACHE[id(enc)] = (enc, {}, {aid: p for p, aid in enumerate(enc.agent_ids)})
+    _, memo, pos = ent
     rows = []
     for panel in portfolio:
-        row = np.zeros(enc.W, np.uint64)
-        ok = True
-        for aid in panel:
-            p = pos.get(aid)
-            if p is None:
-                ok = False
-                break
-            row[p >> 6] |= np.uint64(1) << np.uint64(p & 63)
-        if ok:
+        if isinstance(panel, frozenset):
+            row = memo.get(panel, 0)
+            if row is 0:
+                row = memo[panel] = _pack_one(pos, enc.W, panel)
+        else:
+            row = _pack_one(pos, enc.W, panel)
+        if row is not None:
             rows.append(row)
     if not rows:
         return np.zeros((0, enc.W), np.uint64)
@@ -55,7 +71,7 @@ def first_panel_not_in(enc, k, seed, panel_begin, n_panels, packed_portfolio, ch
 
 def _get_panel_not_in_portfolio_if_possible(categories, agents, k, portfolio, chunk=256):
     """xmin.py:464-474 (same arguments, result and stream consumption)."""
-    enc = encode(categories, agents)
+    enc = encode_cached(categories, agents)
     tries = len(agents) * 3
     first = STREAM.panel
     j, words = first_panel_not_in(enc, k, STREAM.key, first, tries, pack_portfolio(enc, portfolio), chunk=chunk)

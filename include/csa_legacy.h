@@ -189,6 +189,16 @@ int csa_unique_async(const uint64_t *d_hashes, const uint64_t *d_panels, uint64_
 int csa_unique_hashes_async(const uint64_t *d_hashes, uint64_t n_hashes, uint32_t world, uint32_t rank,
                             uint64_t *d_table, uint64_t table_slots, uint64_t *d_unique, void *stream);
 
+/* Histogram of the pair counts d_pairs[i][j], i < j (n*n int64, row-major, as
+ * produced by csa_pair_counts_*): d_hist[v] (n_bins uint64, zeroed by the call)
+ * = number of pairs with count v; pairs with count >= n_bins are counted in
+ * *d_overflow (zeroed by the call).  With n_bins = max person count + 1 nothing
+ * overflows.  The sorted pair probabilities that
+ * plot_pair_probability_distribution_per_algorithm (analysis.py:330-353) draws
+ * are v / S repeated d_hist[v] times, v ascending. */
+int csa_pair_histogram_async(const int64_t *d_pairs, int32_t n, uint64_t *d_hist, uint64_t n_bins,
+                             uint64_t *d_overflow, void *stream);
+
 /* Decode a device status block (host copy of the 4 words) into a CSA_* code
  * and set csa_last_error() accordingly. */
 int csa_status_decode(const uint32_t *h_status);

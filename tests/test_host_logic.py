@@ -122,3 +122,95 @@ def test_pack_portfolio_roundtrip():
     assert rows.shape == (2, enc.W)
     for r, pnl in zip(rows, panels[:2]):
         assert frozenset(enc.agent_ids[p] for p in P.instance.unpack_panel(r, enc.n)) == pnl
+
+
+def _oracle_raw(name, k, S, seed):
+    from oracle import coracle
+    A = pkg("analysis")
+    inst = pkg().read_instance(*inst_paths(name), k)
+    o = oracle_read(*inst_paths(name), k)
+    rc, panels, _, _ = coracle.draw(o, k, seed, 0, S)
+    assert rc == 0
+    raw = A.LegacyRaw(coracle.counts(panels, o.n), coracle.pairs(panels, o.n), coracle.unique(panels, o.n),
+                      panels, None)
+    return inst, raw
+
+
+@pytest.mark.parametrize("keep_panels", [True, False])
+def test_legacy_cache_npz_roundtrip(tmp_path, keep_panels):
+    """cache.save_legacy_npz / load_legacy_npz (run_legacy_or_retrieve, analysis.py:271-293):
+    a retrieved result equals the freshly finished one bit for bit."""
+    A = pkg("analysis")
+    Cc = pkg("cache")
+    S, seed = 3000, 0
+    inst, raw = _oracle_raw("sf_e_110", 110, S, seed)
+    enc = pkg().encode(inst.categories, inst.agents)
+    alloc, found, hist = A.finish(inst, enc, raw, S)
+    path = Cc.legacy_cache_path("sf_e_110", 110, False, tmp_path)
+    assert path.name == "sf_e_110_110_legacy_first.npz"
+    Cc.save_legacy_npz(path, enc, raw, S, seed, 110, keep_panels=keep_panels)
+    alloc2, found2, hist2 = Cc.load_legacy_npz(path, inst)
+    assert alloc2 == alloc
+    assert len(found2) == len(found) == raw.unique
+    assert np.array_equal(hist2.upper(), hist.upper())
+    assert hist2.get_dict() == hist.get_dict()
+    if keep_panels:
+        assert set(found2) == set(found)
+
+
+def test_legacy_cache_rejects_other_instance(tmp_path):
+    Cc = pkg("cache")
+    inst, raw = _oracle_raw("example_small_20", 20, 500, 1)
+    enc = pkg().encode(inst.categories, inst.agents)
+    path = tmp_path / "x.npz"
+    Cc.save_legacy_npz(path, enc, raw, 500, 1, 20)
+    other = pkg().read_instance(*inst_paths("sf_e_110"), 110)
+    with pytest.raises(ValueError):
+        Cc.load_legacy_npz(path, other)
+
+
+@pytest.mark.parametrize("inst", ["example_small_20", "example_large_200",
+                                  "couples_panel_from_twenty_people_no_constraints_2"])
+def test_published_legacy_statistics(inst):
+    """stats.compute_prob_allocation_stats / upper_confidence_bound on the reference's published
+    seed-0 LEGACY allocations (tests/golden/mt_published.json) print the reference's published
+    statistics lines (analysis.py:568-597; tests/golden/published_stats.json)."""
+    import json
+    import os
+    from conftest import GOLD
+    St = pkg("stats")
+    pub = json.load(open(os.path.join(GOLD, "published_stats.json")))[inst]
+    mt = json.load(open(os.path.join(GOLD, "mt_published.json")))[pub["alloc_key"]]
+    alloc = dict(enumerate(mt["selection_probability"]))
+    st = St.compute_prob_allocation_stats(alloc, True)
+    assert f"{st.gini:.1%}" == pub["gini"]
+    assert f"{st.geometric_mean:.1%}" == pub["geometric_mean"]
+    assert f"{St.upper_confidence_bound(10000, float(pub['minimizer_prop'])):.2%}" == pub["ucb"]
+
+
+def test_sorted_counts_to_probabilities():
+    St = pkg("stats")
+    rng = np.random.default_rng(3)
+    counts = rng.integers(0, 50, 1000)
+    hist = np.bincount(counts, minlength=60).astype(np.uint64)
+    S = 977
+    assert St.sorted_counts_to_probabilities(hist, S).tolist() == sorted((c / S for c in counts.tolist()))
+
+
+def test_encode_cached_revalidates():
+    """instance.encode_cached: same dicts -> same encoding; changed counters / agents -> new one."""
+    import copy
+    I = pkg("instance")
+    inst = pkg().read_instance(*inst_paths("example_small_20"), 20)
+    cats, agents = copy.deepcopy(inst.categories), dict(inst.agents)
+    e1 = I.encode_cached(cats, agents)
+    assert I.encode_cached(cats, agents) is e1
+    assert I.encode_cached(copy.deepcopy(cats), agents) is not e1       # other dict object
+    first = next(iter(cats))
+    feat = next(iter(cats[first]))
+    cats[first][feat]["selected"] += 1
+    e2 = I.encode_cached(cats, agents)
+    assert e2 is not e1 and int(e2.sel0.sum()) == 1
+    del agents[0]
+    e3 = I.encode_cached(cats, agents)
+    assert e3 is not e2 and e3.n == 199
