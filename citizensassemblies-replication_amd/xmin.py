@@ -19,6 +19,7 @@ from .legacy import STREAM
 
 
 _ROW_CACHE = {}      # id(enc) -> (enc, {panel: packed row or None}); XMIN's portfolio grows by one per call
+_MISSING = object()
 
 
 def _pack_one(pos, W, panel):
@@ -45,8 +46,8 @@ def pack_portfolio(enc, portfolio):
     rows = []
     for panel in portfolio:
         if isinstance(panel, frozenset):
-            row = memo.get(panel, 0)
-            if row is 0:
+            row = memo.get(panel, _MISSING)
+            if row is _MISSING:
                 row = memo[panel] = _pack_one(pos, enc.W, panel)
         else:
             row = _pack_one(pos, enc.W, panel)
