@@ -118,11 +118,18 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus and rank == 0:
         print("warning: --gpus %d but WORLD_SIZE %d" % (args.gpus, world), file=sys.stderr)
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+    # one process per GPU; the modulo only matters for CSA_BENCH_BACKEND=gloo rehearsals of the
+    # N > 1 path with several ranks on a 1-GPU box (RCCL refuses two ranks on one device)
+    dev_index = local_rank % max(torch.cuda.device_count(), 1)
+    torch.cuda.set_device(dev_index)
+    dev = torch.device("cuda", dev_index)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=dev)
+        backend = os.environ.get("CSA_BENCH_BACKEND", "nccl")     # nccl = RCCL on ROCm
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     P = importlib.import_module(PKG)
     Dv = importlib.import_module(PKG + ".device")
@@ -143,6 +150,7 @@ def main():
     draw_name = pipe.draw_kernel_name()   # the kernel csa_draw_async launches (matches rocprofv3 names)
     stages = ["draw", "hash", "xt_count", "pairs", "unique", "exchange"]
     ev_log = []
+    last = {"unique": pipe.unique}
 
     def step(i, record):
         begin = (i * world + rank) * S            # global panel indices, distinct per step and rank
@@ -168,7 +176,7 @@ def main():
         if evs:
             evs[5].record(stream)
         if world > 1:
-            Dd.combine(pipe.counts, pipe.pairs, pipe.hashes[: 2 * S], table=table, stream=stream)
+            last["unique"] = Dd.combine(pipe.counts, pipe.pairs, pipe.hashes[: 2 * S], table=table, stream=stream)[2]
         if evs:
             evs[6].record(stream)
             ev_log.append(evs)
@@ -255,6 +263,10 @@ def main():
                 kernels["draw"]["pmc_issue"] = pmc["draw_issue"]
                 roof["issue_frac"] = pmc["draw_issue"].get("valu_issue_frac")
 
+    # results of the last step (whole job): a rehearsal of --gpus N --panels P must match a single-GPU
+    # run with --panels N*P (same global panel indices)
+    checks = {"last_step_unique": int(last["unique"].item()), "last_step_count_sum": int(pipe.counts.sum().item()),
+              "last_step_pair_sum": int(pipe.pairs.sum().item()) if want_pairs else None}
     total = S * world * args.steps
     result = {
         "metric": "LEGACY panels/sec (node) at sf_e_110 shape; XtX MFMA util; speedup vs CPU",
@@ -274,6 +286,7 @@ def main():
             "panels_per_gpu_per_step": S, "instance": inst_dir, "parallelism": "panel shards x%d" % world},
         "roofline": roof,
         "kernels": kernels,
+        "checks": checks,
     }
     if want_pairs:
         result["xtx_mfma_util"] = kernels["pairs_mfma"]["mfma_util"]

@@ -894,6 +894,45 @@ __global__ __launch_bounds__(256) void pair_histogram_kernel(const int64_t *__re
     }
 }
 
+// Owner buckets of 128-bit panel hashes for the multi-GPU distinct-panel exchange
+// (owner = h1 % world): pass 1 counts per owner, pass 2 scatters each hash
+// to its owner's range (order inside a bucket is irrelevant to the distinct count).
+constexpr int kMaxWorld = 1024;
+__global__ __launch_bounds__(256) void hash_owner_count_kernel(const uint64_t *__restrict__ hashes, uint64_t n,
+                                                               uint32_t world, unsigned long long *__restrict__ counts) {
+    __shared__ uint32_t c[kMaxWorld];
+    for (uint32_t w = threadIdx.x; w < world; w += blockDim.x) c[w] = 0;
+    __syncthreads();
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+        atomicAdd(&c[hashes[2 * i] % world], 1u);
+    __syncthreads();
+    for (uint32_t w = threadIdx.x; w < world; w += blockDim.x)
+        if (c[w]) atomicAdd(counts + w, (unsigned long long)c[w]);
+}
+
+__global__ __launch_bounds__(256) void hash_owner_scatter_kernel(const uint64_t *__restrict__ hashes, uint64_t n,
+                                                                 uint32_t world,
+                                                                 unsigned long long *__restrict__ cursor,
+                                                                 uint64_t *__restrict__ out) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t h1 = hashes[2 * i], h2 = hashes[2 * i + 1];
+        const unsigned long long pos = atomicAdd(cursor + (h1 % world), 1ull);
+        out[2 * pos] = h1;
+        out[2 * pos + 1] = h2;
+    }
+}
+
+__global__ void exclusive_scan_small_kernel(const unsigned long long *__restrict__ counts, uint32_t world,
+                                            unsigned long long *__restrict__ cursor) {
+    if (threadIdx.x == 0 && blockIdx.x == 0) {
+        unsigned long long acc = 0;
+        for (uint32_t w = 0; w < world; ++w) {
+            cursor[w] = acc;
+            acc += counts[w];
+        }
+    }
+}
+
 // Small-range variant (n_bins <= kHistLdsBins): per-workgroup LDS histogram over a stride of
 // rows (u32 LDS atomics), flushed with one global atomic per non-zero bin -- few distinct values
 // (n = 8192, S = 2e4: ~700 bins for 33.5 M pairs) would otherwise serialise on global atomics.
@@ -1316,6 +1355,31 @@ int csa_pair_histogram_async(const int64_t *d_pairs, int32_t n, uint64_t *d_hist
                            reinterpret_cast<unsigned long long *>(d_overflow));
     }
     HIPCHK(hipGetLastError());
+    return CSA_OK;
+}
+
+int csa_hash_buckets_async(const uint64_t *d_hashes, uint64_t n_hashes, uint32_t world, uint64_t *d_out,
+                           uint64_t *d_counts, uint64_t *d_cursor, void *stream) {
+    if (!d_hashes || !d_out || !d_counts || !d_cursor || world == 0 || world > (uint32_t)kMaxWorld)
+        return fail(CSA_E_INVALID, "hash buckets: bad arguments");
+    hipStream_t st = (hipStream_t)stream;
+    HIPCHK(hipMemsetAsync(d_counts, 0, (size_t)world * 8, st));
+    if (n_hashes) {
+        const unsigned grid = (unsigned)std::min<uint64_t>((n_hashes + 255) / 256, 2048);
+        hipLaunchKernelGGL(hash_owner_count_kernel, dim3(grid), dim3(256), 0, st, d_hashes, n_hashes, world,
+                           reinterpret_cast<unsigned long long *>(d_counts));
+        HIPCHK(hipGetLastError());
+    }
+    hipLaunchKernelGGL(exclusive_scan_small_kernel, dim3(1), dim3(64), 0, st,
+                       reinterpret_cast<const unsigned long long *>(d_counts), world,
+                       reinterpret_cast<unsigned long long *>(d_cursor));
+    HIPCHK(hipGetLastError());
+    if (n_hashes) {
+        const unsigned grid = (unsigned)std::min<uint64_t>((n_hashes + 255) / 256, 2048);
+        hipLaunchKernelGGL(hash_owner_scatter_kernel, dim3(grid), dim3(256), 0, st, d_hashes, n_hashes, world,
+                           reinterpret_cast<unsigned long long *>(d_cursor), d_out);
+        HIPCHK(hipGetLastError());
+    }
     return CSA_OK;
 }
 

@@ -9,10 +9,11 @@ is needed for the draw itself.
 Exchange steps (the only collectives on the path):
   * per-person counts  all_reduce(SUM) int64[n]
   * pair counts        all_reduce(SUM) int64[n*n]   (upper triangle meaningful)
-  * distinct panels    all_gather of every rank's 128-bit panel hashes; rank r
-                       counts the distinct hashes it OWNS (h1 % world == r) with
-                       the device hash table (csa_unique_hashes_async), then
-                       all_reduce(SUM).  Exact within a rank (bitmask compare in
+  * distinct panels    every 128-bit panel hash goes to its OWNER rank
+                       (h1 % world) with one all_to_all (buckets from
+                       csa_hash_buckets_async); the owner counts its distinct
+                       hashes with the device hash table (csa_unique_hashes_async),
+                       then all_reduce(SUM).  Exact within a rank (bitmask compare in
                        the single-rank path); across ranks two panels merge when
                        their 128-bit hashes agree (collision odds ~S^2/2^129).
 On CPU (gloo, tests) the same exchange runs on host tensors and the owner
@@ -84,63 +85,105 @@ def dedupe_hash_partition(all_hashes, world, r):
     return int(len(np.unique(mine, axis=0)))
 
 
-def _gather_hashes(hashes):
-    """all_gather of variable-length int64 hash tensors -> one concatenated tensor."""
-    import torch
-    import torch.distributed as dist
-    world = dist.get_world_size()
-    n_local = torch.tensor([hashes.numel()], dtype=torch.int64, device=hashes.device)
-    sizes = [torch.zeros_like(n_local) for _ in range(world)]
-    dist.all_gather(sizes, n_local)
-    sizes = [int(s.item()) for s in sizes]
-    maxn = max(sizes) if sizes else 0
-    padded = torch.zeros(max(maxn, 1), dtype=torch.int64, device=hashes.device)
-    padded[: hashes.numel()] = hashes
-    gathered = [torch.empty_like(padded) for _ in range(world)]
-    dist.all_gather(gathered, padded)
-    return torch.cat([g[:s] for g, s in zip(gathered, sizes)])
-
-
 class HashTable:
-    """Reusable device table for csa_unique_hashes_async."""
+    """Reusable device table for csa_unique_hashes_async (grows on demand)."""
 
     def __init__(self, max_hashes, device):
         import torch
-        slots = 64
-        while slots < 2 * max(int(max_hashes), 1):
-            slots <<= 1
-        self.slots = slots
-        self.table = torch.empty(slots, dtype=torch.int64, device=device)
+        self.device = device
         self.count = torch.zeros(1, dtype=torch.int64, device=device)
+        self.slots = 0
+        self.ensure(max_hashes)
+
+    def ensure(self, n_hashes):
+        import torch
+        slots = 64
+        while slots < 2 * max(int(n_hashes), 1):
+            slots <<= 1
+        if slots > self.slots:
+            self.slots = slots
+            self.table = torch.empty(slots, dtype=torch.int64, device=self.device)
+
+
+def _host_collectives(t):
+    """gloo has no all_to_all for device tensors: rehearsals (CSA_BENCH_BACKEND=gloo) go via host."""
+    import torch.distributed as dist
+    return t.is_cuda and dist.get_backend() != "nccl"
+
+
+def exchange_hashes(hashes, stream=None):
+    """Send every 128-bit panel hash to its owner rank (h1 % world) with one all_to_all.
+
+    hashes: int64[2*S_local] on the device (buckets from csa_hash_buckets_async) or on the host
+    (numpy bucketing, gloo tests).  Returns int64[2*S_owned], the hashes this rank owns."""
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size()
+    n = hashes.numel() // 2
+    if hashes.is_cuda:
+        from . import _native as N
+        out = torch.empty_like(hashes)
+        counts = torch.empty(world, dtype=torch.int64, device=hashes.device)
+        cursor = torch.empty(world, dtype=torch.int64, device=hashes.device)
+        sp = ctypes.c_void_p((stream or torch.cuda.current_stream(hashes.device)).cuda_stream)
+        N.check(N.lib().csa_hash_buckets_async(N.ptr(hashes), n, world, N.ptr(out), N.ptr(counts), N.ptr(cursor), sp))
+    else:
+        h = hashes.numpy().view(np.uint64).reshape(-1, 2)
+        owner = (h[:, 0] % np.uint64(world)).astype(np.int64)
+        order = np.argsort(owner, kind="stable")
+        out = torch.from_numpy(np.ascontiguousarray(h[order]).view(np.int64).reshape(-1))
+        counts = torch.from_numpy(np.bincount(owner, minlength=world).astype(np.int64))
+    via_host = _host_collectives(out)
+    send_counts = counts.cpu() if via_host else counts
+    recv_counts = torch.empty_like(send_counts)
+    dist.all_to_all_single(recv_counts, send_counts)
+    in_splits = [2 * int(c) for c in send_counts.tolist()]
+    out_splits = [2 * int(c) for c in recv_counts.tolist()]
+    src = out.cpu() if via_host else out
+    recv = torch.empty(sum(out_splits), dtype=torch.int64, device=src.device)
+    dist.all_to_all_single(recv, src, out_splits, in_splits)
+    return recv.to(hashes.device) if via_host else recv
 
 
 def combine(counts, pairs, hashes, table=None, stream=None):
     """Exchange steps for this rank; returns (counts, pairs, unique_tensor).
 
     counts int64[n], pairs int64[n*n] or None, hashes int64[2*S_local] (this rank's
-    panel hashes).  On GPU tensors the owner dedupe runs on the device (``table``
-    = HashTable); on CPU tensors (gloo) it runs in numpy.
+    panel hashes).  Counts and pairs: all_reduce(SUM).  Distinct panels: every hash goes to
+    its owner rank (exchange_hashes, one all_to_all), the owner counts its distinct hashes
+    (device hash table on GPU tensors, numpy on CPU), all_reduce(SUM) of the counts.
     """
     import torch
     import torch.distributed as dist
-    world, r = dist.get_world_size(), dist.get_rank()
-    dist.all_reduce(counts, op=dist.ReduceOp.SUM)
-    if pairs is not None:
-        dist.all_reduce(pairs, op=dist.ReduceOp.SUM)
-    all_h = _gather_hashes(hashes)
-    if all_h.is_cuda:
+    for t in (counts, pairs):
+        if t is None:
+            continue
+        if _host_collectives(t):
+            h = t.cpu()
+            dist.all_reduce(h, op=dist.ReduceOp.SUM)
+            t.copy_(h)
+        else:
+            dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    mine = exchange_hashes(hashes, stream)
+    if mine.is_cuda:
         from . import _native as N
         if table is None:
-            table = HashTable(all_h.numel() // 2, all_h.device)
+            table = HashTable(mine.numel() // 2, mine.device)
+        table.ensure(mine.numel() // 2)
         table.count.zero_()
-        sp = ctypes.c_void_p(stream.cuda_stream) if stream is not None else \
-            ctypes.c_void_p(torch.cuda.current_stream(all_h.device).cuda_stream)
-        N.check(N.lib().csa_unique_hashes_async(N.ptr(all_h), all_h.numel() // 2, world, r, N.ptr(table.table),
+        sp = ctypes.c_void_p((stream or torch.cuda.current_stream(mine.device)).cuda_stream)
+        N.check(N.lib().csa_unique_hashes_async(N.ptr(mine), mine.numel() // 2, 1, 0, N.ptr(table.table),
                                                 table.slots, N.ptr(table.count), sp))
-        u = table.count
+        u = table.count.clone()
     else:
-        u = torch.tensor([dedupe_hash_partition(all_h.numpy().view(np.uint64), world, r)], dtype=torch.int64)
-    dist.all_reduce(u, op=dist.ReduceOp.SUM)
+        m = mine.numpy().view(np.uint64).reshape(-1, 2)
+        u = torch.tensor([int(len(np.unique(m, axis=0))) if len(m) else 0], dtype=torch.int64)
+    if _host_collectives(u):
+        h = u.cpu()
+        dist.all_reduce(h, op=dist.ReduceOp.SUM)
+        u.copy_(h)
+    else:
+        dist.all_reduce(u, op=dist.ReduceOp.SUM)
     return counts, pairs, u
 
 

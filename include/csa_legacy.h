@@ -199,6 +199,15 @@ int csa_unique_hashes_async(const uint64_t *d_hashes, uint64_t n_hashes, uint32_
 int csa_pair_histogram_async(const int64_t *d_pairs, int32_t n, uint64_t *d_hist, uint64_t n_bins,
                              uint64_t *d_overflow, void *stream);
 
+/* Multi-GPU distinct-panel exchange, send side: bucket the 128-bit hashes
+ * (2*n_hashes uint64) by owner rank h1 % world into d_out (2*n_hashes uint64,
+ * owner-major, any order inside a bucket); d_counts (world uint64) = hashes
+ * per owner, d_cursor (world uint64) scratch.  The buckets feed an
+ * all_to_all; each rank then counts its received hashes with
+ * csa_unique_hashes_async(world = 1, rank = 0).  world <= 1024. */
+int csa_hash_buckets_async(const uint64_t *d_hashes, uint64_t n_hashes, uint32_t world, uint64_t *d_out,
+                           uint64_t *d_counts, uint64_t *d_cursor, void *stream);
+
 /* Decode a device status block (host copy of the 4 words) into a CSA_* code
  * and set csa_last_error() accordingly. */
 int csa_status_decode(const uint32_t *h_status);

@@ -247,3 +247,29 @@ def test_device_hashes_match_host_mirror(gpu_available):
     pipe.check_status()
     dev_h = pipe.hashes.cpu().numpy().view(np.uint64).reshape(-1, 2)
     assert np.array_equal(dev_h, D.panel_hashes(pipe.panels_view(4096)))
+
+
+@pytest.mark.parametrize("world", [1, 3, 8])
+def test_hash_buckets(gpu_available, world):
+    """csa_hash_buckets_async: owner-major buckets (h1 % world) holding exactly the input hashes."""
+    import torch
+    N = pkg("_native")
+    rng = np.random.default_rng(world)
+    h = rng.integers(0, 2 ** 63, size=(50001, 2), dtype=np.int64)
+    d = torch.from_numpy(h.reshape(-1)).cuda()
+    out = torch.empty_like(d)
+    counts = torch.empty(world, dtype=torch.int64, device="cuda")
+    cursor = torch.empty(world, dtype=torch.int64, device="cuda")
+    N.check(N.lib().csa_hash_buckets_async(N.ptr(d), 50001, world, N.ptr(out), N.ptr(counts), N.ptr(cursor), None))
+    torch.cuda.synchronize()
+    o = out.cpu().numpy().reshape(-1, 2).view(np.uint64)
+    owner = h.view(np.uint64)[:, 0] % np.uint64(world)
+    c = counts.cpu().numpy()
+    assert c.tolist() == np.bincount(owner.astype(np.int64), minlength=world).tolist()
+    start = 0
+    for w in range(world):
+        seg = o[start:start + c[w]]
+        assert np.all(seg[:, 0] % np.uint64(world) == np.uint64(w))
+        want = h.view(np.uint64)[owner == np.uint64(w)]
+        assert sorted(map(tuple, seg.tolist())) == sorted(map(tuple, want.tolist()))
+        start += c[w]
