@@ -523,6 +523,7 @@ __global__ __launch_bounds__(kDrawThreads, draw_occupancy(FPL, WPL)) void draw_k
 }
 
 #include "draw_batch.inc"
+#include "draw_lane.inc"
 
 // 128-bit panel hashes (the draw_kernel's in-kernel hash, for the batch kernel's panels): a
 // quad of lanes per panel, words glane, glane+4, ... (coalesced within the quad), quad sum.
@@ -632,7 +633,7 @@ typedef float v16f __attribute__((ext_vector_type(16)));
 
 constexpr int kPairBlock = 256;   // output block per workgroup
 constexpr int kPairThreads = 512;
-constexpr int kPairKB = 4;        // 64-panel blocks staged per barrier
+constexpr int kPairKB = 4;        // default 64-panel blocks staged per barrier (template KB)
 
 // int8 fragment (k-half ks, lane half h) of one XT word: dword q holds bits 4h+q, 4h+q+8,
 // 4h+q+16, 4h+q+24 of the 32-bit half ks as 0/1 bytes.  Any fixed bit -> k placement works
@@ -679,17 +680,27 @@ __device__ __forceinline__ void tri_block(int tri, int nbt, int &bi, int &bj) {
     bj = bi + rem;
 }
 
-template <bool FP4, bool PARTIAL>
+template <bool FP4, bool PARTIAL, int KB>
 __global__ __launch_bounds__(kPairThreads) void pair_mfma_kernel(const uint64_t *__restrict__ xt,
                                                                  uint64_t nblk, int n, int npad,
                                                                  int nbt, int nsplit,
                                                                  int64_t *__restrict__ pairs,
-                                                                 int32_t *__restrict__ part) {
-    constexpr int KB = kPairKB;
+                                                                 int32_t *__restrict__ part, int xcd_map) {
     __shared__ uint64_t words[2][KB][2 * kPairBlock];
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-    const int item = blockIdx.x;
-    const int tri = item / nsplit, split = item - tri * nsplit;
+    int tri, split;
+    if (xcd_map) {
+        // workgroups are dispatched round-robin over the 8 XCDs (blockIdx % 8): give every
+        // workgroup of one XCD the same panel-block split (nsplit % 8 == 0), so the 7-fold re-reads
+        // of each XT row block by the triangle blocks of that split hit the XCD's own L2
+        const int ntri = nbt * (nbt + 1) / 2, r = (int)(blockIdx.x >> 3);
+        tri = r % ntri;
+        split = (int)(blockIdx.x & 7) + 8 * (r / ntri);
+    } else {
+        tri = (int)blockIdx.x / nsplit;
+        split = (int)blockIdx.x - tri * nsplit;
+    }
+    const int item = tri * nsplit + split;
     int bi, bj;
     tri_block(tri, nbt, bi, bj);
     const int I0 = bi * kPairBlock, J0 = bj * kPairBlock;
@@ -1016,8 +1027,44 @@ int check_k(const csa_instance *I, int32_t k) {
 struct DrawConfig {
     int G = 16, FPL = 1, WPL = 1;
     bool batch = false;  // draw_batch_kernel (small groups) instead of draw_kernel
+    bool lane = false;   // draw_lane_kernel (G = 1): FPL / WPL hold its FN / WN
     const void *fn = nullptr;
 };
+
+template <int G, int FN>
+const void *lane_fn_w(int wn) {
+    if constexpr (FN / G < 4) {
+        return nullptr;
+    } else {
+        switch (wn) {
+            case 4: return reinterpret_cast<const void *>(&draw_lane_kernel<G, FN, 4>);
+            case 8: return reinterpret_cast<const void *>(&draw_lane_kernel<G, FN, 8>);
+            case 16: return reinterpret_cast<const void *>(&draw_lane_kernel<G, FN, 16>);
+            case 28: return reinterpret_cast<const void *>(&draw_lane_kernel<G, FN, 28>);
+            case 32: return reinterpret_cast<const void *>(&draw_lane_kernel<G, FN, 32>);
+            default: return nullptr;
+        }
+    }
+}
+
+template <int G>
+const void *lane_fn_g(int fn_, int wn) {
+    switch (fn_) {
+        case 8: return lane_fn_w<G, 8>(wn);
+        case 16: return lane_fn_w<G, 16>(wn);
+        case 32: return lane_fn_w<G, 32>(wn);
+        default: return nullptr;
+    }
+}
+
+const void *lane_fn(int g, int fn_, int wn) {
+    switch (g) {
+        case 1: return lane_fn_g<1>(fn_, wn);
+        case 2: return lane_fn_g<2>(fn_, wn);
+        case 4: return lane_fn_g<4>(fn_, wn);
+        default: return nullptr;
+    }
+}
 
 template <int G, int FPL, int WPL, bool GEN>
 const void *draw_fn() {
@@ -1074,8 +1121,9 @@ int pow2_ceil_int(int x) {
     return p;
 }
 
-// Batch draws: draw_batch_kernel with G = 4 lanes per panel (16 panels per wavefront) when the
-// instance fits (F <= 32, W <= 32), else draw_kernel with G = 16 (F <= 64) or 64.
+// Batch draws: draw_lane_kernel with G = 2 lanes per panel (32 panels per wavefront) when the
+// instance fits (F <= 32, W <= 32, no max = 0 < min feature), else draw_kernel with G = 16
+// (F <= 64) or 64.  draw_batch_kernel (G = 4 / 8) stays selectable.
 // CSA_DRAW_GROUP=4|8|16|64 overrides (benchmarking).  Pick-order / single-attempt draws
 // (general mode) use the G = 64 draw_kernel.
 int pick_draw_config(const csa_instance *I, bool general, DrawConfig &c) {
@@ -1083,7 +1131,25 @@ int pick_draw_config(const csa_instance *I, bool general, DrawConfig &c) {
     int G = general ? 64 : (small && I->W <= 32) ? 4 : (I->F <= 64 && I->W <= 256) ? 16 : 64;
     if (const char *e = getenv("CSA_DRAW_GROUP")) {
         const int g = atoi(e);
-        if (!general && (g == 16 || g == 64 || (small && (g == 4 || g == 8)))) G = g;
+        if (!general && (g == 16 || g == 64 || (small && (g == 4 || g == 8)) || (small && g == 1 && I->W <= 32)))
+            G = g;
+    }
+    // draw_lane_kernel group size: 2 lanes per panel by default (fastest at sf_e: 6.06 ms / 10^6
+    // panels vs 7.47 for G = 1 and draw_batch_kernel<4>, 6.30 for G = 4); CSA_DRAW_GROUP=4|8|16|64
+    // selects the other kernels, CSA_DRAW_GROUP=1 / CSA_DRAW_LANE=1|2|4 the lane kernel's G
+    int lane_g = 2;
+    if (const char *e = getenv("CSA_DRAW_GROUP")) lane_g = atoi(e) == 1 ? 1 : 0;
+    if (const char *e = getenv("CSA_DRAW_LANE")) lane_g = atoi(e);
+    if (!general && small && I->W <= 32 && (lane_g == 1 || lane_g == 2 || lane_g == 4)) {
+        // draw_lane_kernel: FN in {8, 16, 32} (FN / G >= 4), WN in {4, 8, 16, 28, 32}
+        c.G = lane_g;
+        c.lane = true;
+        c.batch = false;
+        c.FPL = std::max({8, 4 * lane_g, pow2_ceil_int(I->F)});
+        c.WPL = I->W <= 4 ? 4 : I->W <= 8 ? 8 : I->W <= 16 ? 16 : I->W <= 28 ? 28 : 32;
+        c.fn = lane_fn(lane_g, c.FPL, c.WPL);
+        if (!c.fn) return fail(CSA_E_UNSUPPORTED, "no lane draw kernel for G=%d F=%d W=%d", lane_g, I->F, I->W);
+        return CSA_OK;
     }
     c.G = G;
     c.batch = G <= 8;
@@ -1141,10 +1207,11 @@ int launch_draw(const csa_instance *I, int32_t k, uint64_t seed, uint64_t panel_
     A.sel_out = d_sel_out;
     A.rem_out = d_rem_out;
     A.present_out = d_present_out;
-    const int threads = cfg.batch ? kBatchThreads : kDrawThreads;
+    const int threads = cfg.lane ? kLaneThreads : cfg.batch ? kBatchThreads : kDrawThreads;
     const int groups_wg = threads / cfg.G;
-    const size_t lds = cfg.batch ? batch_lds_bytes(cfg.G, cfg.FPL, cfg.WPL, I->n, I->W, k, groups_wg)
-                                 : draw_lds_bytes(cfg.G, cfg.FPL, cfg.WPL, I->W, k, groups_wg);
+    const size_t lds = cfg.lane    ? lane_lds_bytes(cfg.FPL, cfg.WPL, I->n)
+                       : cfg.batch ? batch_lds_bytes(cfg.G, cfg.FPL, cfg.WPL, I->n, I->W, k, groups_wg)
+                                   : draw_lds_bytes(cfg.G, cfg.FPL, cfg.WPL, I->W, k, groups_wg);
     if (lds > 160 * 1024) return fail(CSA_E_UNSUPPORTED, "draw kernel needs %zu B of LDS", lds);
     int per_cu = 0, cus = 0;
     HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, cfg.fn, threads, lds));
@@ -1155,7 +1222,7 @@ int launch_draw(const csa_instance *I, int32_t k, uint64_t seed, uint64_t panel_
     void *args[] = {&A};
     HIPCHK(hipLaunchKernel(cfg.fn, dim3(grid), dim3(threads), args, lds, stream));
     HIPCHK(hipGetLastError());
-    if (cfg.batch && d_hashes) {  // the batch kernel leaves hashing to a streaming pass
+    if ((cfg.batch || cfg.lane) && d_hashes) {  // batch / lane kernels leave hashing to a streaming pass
         hipLaunchKernelGGL(panel_hash_kernel, dim3((unsigned)((n_panels * 4 + 255) / 256)), dim3(256), 0, stream,
                            d_panels, n_panels, I->W, d_hashes);
         HIPCHK(hipGetLastError());
@@ -1426,8 +1493,11 @@ int csa_draw_kernel_name(const csa_instance *I, int32_t k, char *buf, uint64_t l
     DrawConfig cfg;
     rc = pick_draw_config(I, false, cfg);
     if (rc) return rc;
-    snprintf(buf, (size_t)len, "%s<%d, %d, %d%s>", cfg.batch ? "draw_batch_kernel" : "draw_kernel", cfg.G, cfg.FPL,
-             cfg.WPL, cfg.batch ? "" : ", false");
+    if (cfg.lane)
+        snprintf(buf, (size_t)len, "draw_lane_kernel<%d, %d, %d>", cfg.G, cfg.FPL, cfg.WPL);
+    else
+        snprintf(buf, (size_t)len, "%s<%d, %d, %d%s>", cfg.batch ? "draw_batch_kernel" : "draw_kernel", cfg.G,
+                 cfg.FPL, cfg.WPL, cfg.batch ? "" : ", false");
     return CSA_OK;
 }
 
@@ -1450,7 +1520,7 @@ int csa_transpose_count_async(const uint64_t *d_panels, uint64_t n_panels, int32
 
 namespace {
 struct PairPlan {
-    int npad, nbt, ntri, nsplit;
+    int npad, nbt, ntri, nsplit, xcd_map;
 };
 
 // one 512-thread workgroup per CU (two waves per SIMD): fill the CUs once, keep >= 8 panel
@@ -1468,6 +1538,18 @@ int pair_plan(int32_t n, uint64_t n_blocks, uint32_t engine, PairPlan &p) {
     const uint64_t exact_blocks = engine == CSA_PAIR_FP4 ? (1ull << 24) / 64 : (1ull << 31) / 64;
     ns = std::max<uint64_t>(ns, (n_blocks + exact_blocks - 1) / exact_blocks);
     if (ns > (1u << 20)) return fail(CSA_E_UNSUPPORTED, "pairs: too many panel blocks per call");
+    // XCD-aware split mapping (pair_mfma_kernel; CSA_PAIR_XCD=1) when there are >= 8 splits: round
+    // down to a multiple of 8 unless that breaks the exactness bound.  Off by default: at sf_e it
+    // leaves 32 CUs idle (224 workgroups) and measured 0.90 vs 0.82 ms.
+    p.xcd_map = 0;
+    const char *ex = getenv("CSA_PAIR_XCD");
+    if (ns >= 8 && ex && atoi(ex) == 1) {
+        const uint64_t ns8 = ns / 8 * 8;
+        if (ns8 * exact_blocks >= n_blocks) {
+            ns = ns8;
+            p.xcd_map = 1;
+        }
+    }
     p.nsplit = (int)ns;
     return CSA_OK;
 }
@@ -1493,21 +1575,23 @@ int csa_pair_counts_ex_async(const uint64_t *d_xt, uint64_t n_blocks, int32_t n,
     const dim3 grid(p.ntri * p.nsplit), block(kPairThreads);
     int32_t *part = static_cast<int32_t *>(d_scratch);
     const hipStream_t st = (hipStream_t)stream;
-    if (engine == CSA_PAIR_FP4) {
-        if (partial)
-            hipLaunchKernelGGL((pair_mfma_kernel<true, true>), grid, block, 0, st, d_xt, n_blocks, n, p.npad, p.nbt,
-                               p.nsplit, d_pairs, part);
-        else
-            hipLaunchKernelGGL((pair_mfma_kernel<true, false>), grid, block, 0, st, d_xt, n_blocks, n, p.npad, p.nbt,
-                               p.nsplit, d_pairs, part);
-    } else {
-        if (partial)
-            hipLaunchKernelGGL((pair_mfma_kernel<false, true>), grid, block, 0, st, d_xt, n_blocks, n, p.npad, p.nbt,
-                               p.nsplit, d_pairs, part);
-        else
-            hipLaunchKernelGGL((pair_mfma_kernel<false, false>), grid, block, 0, st, d_xt, n_blocks, n, p.npad,
-                               p.nbt, p.nsplit, d_pairs, part);
-    }
+    // panel blocks staged per barrier (prefetch distance): CSA_PAIR_KB = 4 / 8 / 16 overrides
+    int kb = kPairKB;
+    if (const char *e = getenv("CSA_PAIR_KB")) kb = atoi(e);
+    const void *fn = nullptr;
+#define CSA_PAIR_FN(F4, PA)                                                                       \
+    (kb == 16 ? reinterpret_cast<const void *>(&pair_mfma_kernel<F4, PA, 16>)                     \
+              : kb == 8 ? reinterpret_cast<const void *>(&pair_mfma_kernel<F4, PA, 8>)            \
+                        : reinterpret_cast<const void *>(&pair_mfma_kernel<F4, PA, 4>))
+    if (engine == CSA_PAIR_FP4)
+        fn = partial ? CSA_PAIR_FN(true, true) : CSA_PAIR_FN(true, false);
+    else
+        fn = partial ? CSA_PAIR_FN(false, true) : CSA_PAIR_FN(false, false);
+#undef CSA_PAIR_FN
+    uint64_t nb = n_blocks;
+    int npad = p.npad, nbt = p.nbt, nsplit = p.nsplit, xcd = p.xcd_map;
+    void *args[] = {(void *)&d_xt, &nb, &n, &npad, &nbt, &nsplit, &d_pairs, &part, &xcd};
+    HIPCHK(hipLaunchKernel(fn, grid, block, args, 0, st));
     HIPCHK(hipGetLastError());
     if (partial) {
         hipLaunchKernelGGL(pair_reduce_kernel, dim3(kPairBlock, p.ntri), dim3(256), 0, st, part, n, p.nbt, p.nsplit,

@@ -19,12 +19,25 @@ pytestmark = pytest.mark.gpu
 
 @pytest.fixture
 def draw_group():
-    old = os.environ.get("CSA_DRAW_GROUP")
-    yield lambda g: os.environ.__setitem__("CSA_DRAW_GROUP", str(g))
-    if old is None:
-        os.environ.pop("CSA_DRAW_GROUP", None)
-    else:
-        os.environ["CSA_DRAW_GROUP"] = old
+    """Force a draw layout: an int G selects CSA_DRAW_GROUP=G (batch / general kernels, 1 = lane
+    kernel with one lane per panel); "2L" / "4L" select the lane kernel with 2 / 4 lanes per panel
+    (CSA_DRAW_LANE)."""
+    names = ("CSA_DRAW_GROUP", "CSA_DRAW_LANE")
+    old = {k: os.environ.get(k) for k in names}
+
+    def set_layout(g):
+        for k in names:
+            os.environ.pop(k, None)
+        if isinstance(g, str) and g.endswith("L"):
+            os.environ["CSA_DRAW_LANE"] = g[:-1]
+        else:
+            os.environ["CSA_DRAW_GROUP"] = str(g)
+    yield set_layout
+    for k, v in old.items():
+        if v is None:
+            os.environ.pop(k, None)
+        else:
+            os.environ[k] = v
 
 
 def _sample(enc, k, S, seed, begin=0, max_attempts=0):
@@ -36,7 +49,7 @@ def _sample(enc, k, S, seed, begin=0, max_attempts=0):
     return panels, attempts
 
 
-@pytest.mark.parametrize("group", [4, 8, 16, 64])
+@pytest.mark.parametrize("group", [1, "2L", "4L", 4, 8, 16, 64])
 @pytest.mark.parametrize("name,k,S,seed", [("sf_e_tight_110", 110, 3000, 5), ("pathological_5", 5, 4000, 2),
                                            ("rejecty_6", 6, 20000, 8), ("example_small_20", 20, 20000, 1),
                                            ("couples_panel_from_twenty_people_no_constraints_2", 2, 20000, 3)])
@@ -64,7 +77,7 @@ def _weird_instance():
     return cats, agents
 
 
-@pytest.mark.parametrize("group", [4, 8, 16, 64])
+@pytest.mark.parametrize("group", [1, "2L", "4L", 4, 8, 16, 64])
 def test_zero_max_features_match_oracle(gpu_available, draw_group, group):
     """max = 0 features (dead, and max = 0 < min which routes to draw_kernel) vs the oracle."""
     P = pkg()
