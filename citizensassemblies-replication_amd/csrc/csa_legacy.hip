@@ -1209,7 +1209,7 @@ int launch_draw(const csa_instance *I, int32_t k, uint64_t seed, uint64_t panel_
     A.present_out = d_present_out;
     const int threads = cfg.lane ? kLaneThreads : cfg.batch ? kBatchThreads : kDrawThreads;
     const int groups_wg = threads / cfg.G;
-    const size_t lds = cfg.lane    ? lane_lds_bytes(cfg.FPL, cfg.WPL, I->n)
+    const size_t lds = cfg.lane    ? lane_lds_bytes(cfg.G, cfg.FPL, cfg.WPL, I->n)
                        : cfg.batch ? batch_lds_bytes(cfg.G, cfg.FPL, cfg.WPL, I->n, I->W, k, groups_wg)
                                    : draw_lds_bytes(cfg.G, cfg.FPL, cfg.WPL, I->W, k, groups_wg);
     if (lds > 160 * 1024) return fail(CSA_E_UNSUPPORTED, "draw kernel needs %zu B of LDS", lds);
