@@ -1140,7 +1140,8 @@ int pick_draw_config(const csa_instance *I, bool general, DrawConfig &c) {
     int lane_g = 2;
     if (const char *e = getenv("CSA_DRAW_GROUP")) lane_g = atoi(e) == 1 ? 1 : 0;
     if (const char *e = getenv("CSA_DRAW_LANE")) lane_g = atoi(e);
-    if (!general && small && I->W <= 32 && (lane_g == 1 || lane_g == 2 || lane_g == 4)) {
+    // the lane kernel packs need and remaining as 16-bit halves: |min|, |selected| < 2^15 (n <= 16384)
+    if (!general && small && I->W <= 32 && I->max_abs < 32768 && (lane_g == 1 || lane_g == 2 || lane_g == 4)) {
         // draw_lane_kernel: FN in {8, 16, 32} (FN / G >= 4), WN in {4, 8, 16, 28, 32}
         c.G = lane_g;
         c.lane = true;
