@@ -646,11 +646,10 @@ __device__ __forceinline__ v4i i8_frag(uint64_t w, int ks, int h) {
     return r;
 }
 
-// fp4 fragments of the 32 bits x = word >> 32h (lane half h covers k = 32h .. 32h+31):
+// fp4 fragments of the 32 bits x = half h of a word (lane half h covers k = 32h .. 32h+31):
 // bit 4i+p of x goes to nibble i of dword p (A: positions 0,1,2,2 -> 0.5,1,2,2;
 // B: positions 2,1,0,0 -> 2,1,0.5,0.5).
-__device__ __forceinline__ v8i f4_frag_a(uint64_t w, int h) {
-    const uint32_t x = (uint32_t)(w >> (32 * h));
+__device__ __forceinline__ v8i f4_frag_a(uint32_t x) {
     v8i r;
     r[0] = (int)(x & 0x11111111u);
     r[1] = (int)(x & 0x22222222u);
@@ -659,8 +658,7 @@ __device__ __forceinline__ v8i f4_frag_a(uint64_t w, int h) {
     r[4] = r[5] = r[6] = r[7] = 0;  // fp4 operands use 4 registers
     return r;
 }
-__device__ __forceinline__ v8i f4_frag_b(uint64_t w, int h) {
-    const uint32_t x = (uint32_t)(w >> (32 * h));
+__device__ __forceinline__ v8i f4_frag_b(uint32_t x) {
     v8i r;
     r[0] = (int)((x << 2) & 0x44444444u);
     r[1] = (int)(x & 0x22222222u);
@@ -741,17 +739,14 @@ __global__ __launch_bounds__(kPairThreads) void pair_mfma_kernel(const uint64_t 
         for (int j = 0; j < KB; ++j) {
             {  // branch-free: the tail stage's missing blocks are zero words
                 const uint64_t *w = words[buf][j];
-                uint64_t wa[4], wb[2];
-#pragma unroll
-                for (int x = 0; x < 4; ++x) wa[x] = w[128 * wr + 32 * x + r32];
-#pragma unroll
-                for (int x = 0; x < 2; ++x) wb[x] = w[kPairBlock + 64 * wc + 32 * x + r32];
                 if constexpr (FP4) {
+                    // lane half h needs only the 32-bit half h of each word: read it directly
+                    const uint32_t *w32 = reinterpret_cast<const uint32_t *>(w) + h;
                     v8i fa[4], fb[2];
 #pragma unroll
-                    for (int x = 0; x < 4; ++x) fa[x] = f4_frag_a(wa[x], h);
+                    for (int x = 0; x < 4; ++x) fa[x] = f4_frag_a(w32[2 * (128 * wr + 32 * x + r32)]);
 #pragma unroll
-                    for (int x = 0; x < 2; ++x) fb[x] = f4_frag_b(wb[x], h);
+                    for (int x = 0; x < 2; ++x) fb[x] = f4_frag_b(w32[2 * (kPairBlock + 64 * wc + 32 * x + r32)]);
 #pragma unroll
                     for (int a = 0; a < 4; ++a)
 #pragma unroll
@@ -759,6 +754,11 @@ __global__ __launch_bounds__(kPairThreads) void pair_mfma_kernel(const uint64_t 
                             acc[a][b] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(
                                 fa[a], fb[b], acc[a][b], 4, 4, 0, 0x7F7F7F7F, 0, 0x7F7F7F7F);
                 } else {
+                    uint64_t wa[4], wb[2];
+#pragma unroll
+                    for (int x = 0; x < 4; ++x) wa[x] = w[128 * wr + 32 * x + r32];
+#pragma unroll
+                    for (int x = 0; x < 2; ++x) wb[x] = w[kPairBlock + 64 * wc + 32 * x + r32];
 #pragma unroll
                     for (int ks = 0; ks < 2; ++ks) {
                         v4i fa[4], fb[2];
