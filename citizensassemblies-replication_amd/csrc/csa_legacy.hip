@@ -818,6 +818,124 @@ __global__ __launch_bounds__(kPairThreads) void pair_mfma_kernel(const uint64_t 
 
 // Sum the nsplit int32 partial tiles of every upper-triangular block into the int64 output
 // (+=; each output element is owned by exactly one thread).  HBM-bound.
+// Wide variant of the fp4 engine: 4 waves per workgroup, each a 128 x 128 tile (4 x 4
+// accumulators = 256 accumulation registers, one wave per SIMD), so a word's 8 fragments feed 16
+// MFMAs (0.5 fragments per MFMA instead of 0.75): the fragment expansion is the VALU cost that
+// bounds pair_mfma_kernel.  Same staging, partial blocks and exactness bound.
+template <bool PARTIAL, int KB>
+__global__ __launch_bounds__(256, 1) void pair_mfma_wide_kernel(const uint64_t *__restrict__ xt, uint64_t nblk, int n,
+                                                                int npad, int nbt, int nsplit,
+                                                                int64_t *__restrict__ pairs,
+                                                                int32_t *__restrict__ part, int xcd_map) {
+    __shared__ uint64_t words[2][KB][2 * kPairBlock];
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    int tri, split;
+    if (xcd_map) {
+        const int ntri = nbt * (nbt + 1) / 2, r = (int)(blockIdx.x >> 3);
+        tri = r % ntri;
+        split = (int)(blockIdx.x & 7) + 8 * (r / ntri);
+    } else {
+        tri = (int)blockIdx.x / nsplit;
+        split = (int)blockIdx.x - tri * nsplit;
+    }
+    const int item = tri * nsplit + split;
+    int bi, bj;
+    tri_block(tri, nbt, bi, bj);
+    const int I0 = bi * kPairBlock, J0 = bj * kPairBlock;
+    const uint64_t per = (nblk + nsplit - 1) / nsplit;
+    const uint64_t kb0 = min(nblk, (uint64_t)split * per), kb1 = min(nblk, kb0 + per);
+
+    v16f acc[4][4];
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b)
+#pragma unroll
+            for (int v = 0; v < 16; ++v) acc[a][b][v] = 0.0f;
+
+    const int wr = wave >> 1, wc = wave & 1;
+    const int r32 = lane & 31, h = lane >> 5;
+    uint64_t nwr[KB], nwc[KB];  // this thread stages row word I0 + t and column word J0 + t
+    const uint64_t nst = (kb1 - kb0 + KB - 1) / KB;
+    auto load_stage = [&](uint64_t s) {
+#pragma unroll
+        for (int j = 0; j < KB; ++j) {  // blocks past the split's end stage as zero words
+            const uint64_t b = kb0 + s * KB + j;
+            nwr[j] = b < kb1 ? xt[b * (uint64_t)npad + I0 + t] : 0ull;
+            nwc[j] = b < kb1 ? xt[b * (uint64_t)npad + J0 + t] : 0ull;
+        }
+    };
+    if (nst) {
+        load_stage(0);
+#pragma unroll
+        for (int j = 0; j < KB; ++j) {
+            words[0][j][t] = nwr[j];
+            words[0][j][kPairBlock + t] = nwc[j];
+        }
+        if (nst > 1) load_stage(1);
+    }
+    __syncthreads();
+    for (uint64_t s = 0; s < nst; ++s) {
+        const int buf = (int)(s & 1);
+#pragma unroll
+        for (int j = 0; j < KB; ++j) {
+            const uint32_t *w32 = reinterpret_cast<const uint32_t *>(words[buf][j]) + h;
+            v8i fa[4], fb[4];
+#pragma unroll
+            for (int x = 0; x < 4; ++x) fa[x] = f4_frag_a(w32[2 * (128 * wr + 32 * x + r32)]);
+#pragma unroll
+            for (int y = 0; y < 4; ++y) fb[y] = f4_frag_b(w32[2 * (kPairBlock + 128 * wc + 32 * y + r32)]);
+#pragma unroll
+            for (int a = 0; a < 4; ++a)
+#pragma unroll
+                for (int b = 0; b < 4; ++b)
+                    acc[a][b] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(fa[a], fb[b], acc[a][b], 4, 4, 0,
+                                                                                0x7F7F7F7F, 0, 0x7F7F7F7F);
+            if (j == 0) {  // hand the prefetched stage to LDS, prefetch the one after
+                if (s + 1 < nst) {
+#pragma unroll
+                    for (int jj = 0; jj < KB; ++jj) {
+                        words[buf ^ 1][jj][t] = nwr[jj];
+                        words[buf ^ 1][jj][kPairBlock + t] = nwc[jj];
+                    }
+                }
+                if (s + 2 < nst) load_stage(s + 2);
+            }
+        }
+        __syncthreads();
+    }
+    // C/D layout (gfx950): col = lane & 31, row = (v&3) + 8*(v>>2) + 4*(lane>>5)
+    const int rloc = 128 * wr + 4 * h, cloc = 128 * wc + r32;
+    if constexpr (PARTIAL) {
+        int32_t *dst = part + (size_t)item * kPairBlock * kPairBlock;
+#pragma unroll
+        for (int a = 0; a < 4; ++a)
+#pragma unroll
+            for (int b = 0; b < 4; ++b)
+#pragma unroll
+                for (int v = 0; v < 16; ++v) {
+                    const int row = rloc + 32 * a + (v & 3) + 8 * (v >> 2);
+                    dst[row * kPairBlock + cloc + 32 * b] = (int)acc[a][b][v];
+                }
+    } else {
+#pragma unroll
+        for (int a = 0; a < 4; ++a)
+#pragma unroll
+            for (int b = 0; b < 4; ++b) {
+                const int col = J0 + cloc + 32 * b;
+#pragma unroll
+                for (int v = 0; v < 16; ++v) {
+                    const int row = I0 + rloc + 32 * a + (v & 3) + 8 * (v >> 2);
+                    const int val = (int)acc[a][b][v];
+                    if (val != 0 && row < n && col < n)
+                        atomicAdd(reinterpret_cast<unsigned long long *>(pairs + (uint64_t)row * n + col),
+                                  (unsigned long long)(long long)val);
+                }
+                __builtin_amdgcn_sched_barrier(0);
+            }
+    }
+}
+
 __global__ __launch_bounds__(256) void pair_reduce_kernel(const int32_t *__restrict__ part, int n, int nbt,
                                                           int nsplit, int64_t *__restrict__ pairs) {
     int bi, bj;
@@ -1586,7 +1704,18 @@ int csa_pair_counts_ex_async(const uint64_t *d_xt, uint64_t n_blocks, int32_t n,
     (kb == 16 ? reinterpret_cast<const void *>(&pair_mfma_kernel<F4, PA, 16>)                     \
               : kb == 8 ? reinterpret_cast<const void *>(&pair_mfma_kernel<F4, PA, 8>)            \
                         : reinterpret_cast<const void *>(&pair_mfma_kernel<F4, PA, 4>))
-    if (engine == CSA_PAIR_FP4)
+    // fp4 engine, CSA_PAIR_WIDE=1: the wide kernel (4 waves of 128 x 128, one wave per SIMD).
+    // Off by default: 0.71 vs 0.64 ms at sf_e -- one wave per SIMD hides the LDS/VALU latency worse
+    bool wide = false;
+    if (const char *e = getenv("CSA_PAIR_WIDE")) wide = engine == CSA_PAIR_FP4 && atoi(e) != 0;
+    if (wide)
+        fn = kb == 16 ? (partial ? reinterpret_cast<const void *>(&pair_mfma_wide_kernel<true, 16>)
+                                 : reinterpret_cast<const void *>(&pair_mfma_wide_kernel<false, 16>))
+             : kb == 4 ? (partial ? reinterpret_cast<const void *>(&pair_mfma_wide_kernel<true, 4>)
+                                  : reinterpret_cast<const void *>(&pair_mfma_wide_kernel<false, 4>))
+                       : (partial ? reinterpret_cast<const void *>(&pair_mfma_wide_kernel<true, 8>)
+                                  : reinterpret_cast<const void *>(&pair_mfma_wide_kernel<false, 8>));
+    else if (engine == CSA_PAIR_FP4)
         fn = partial ? CSA_PAIR_FN(true, true) : CSA_PAIR_FN(true, false);
     else
         fn = partial ? CSA_PAIR_FN(false, true) : CSA_PAIR_FN(false, false);
@@ -1594,7 +1723,7 @@ int csa_pair_counts_ex_async(const uint64_t *d_xt, uint64_t n_blocks, int32_t n,
     uint64_t nb = n_blocks;
     int npad = p.npad, nbt = p.nbt, nsplit = p.nsplit, xcd = p.xcd_map;
     void *args[] = {(void *)&d_xt, &nb, &n, &npad, &nbt, &nsplit, &d_pairs, &part, &xcd};
-    HIPCHK(hipLaunchKernel(fn, grid, block, args, 0, st));
+    HIPCHK(hipLaunchKernel(fn, grid, wide ? dim3(256) : block, args, 0, st));
     HIPCHK(hipGetLastError());
     if (partial) {
         hipLaunchKernelGGL(pair_reduce_kernel, dim3(kPairBlock, p.ntri), dim3(256), 0, st, part, n, p.nbt, p.nsplit,
