@@ -118,6 +118,8 @@ def test_full_size_properties_sf_e(gpu_available):
     assert np.array_equal(full.sum(axis=1), (k - 1) * raw.counts)
     assert np.array_equal(np.diag(raw.pairs), raw.counts)
     assert raw.unique <= S
+    # the distinct count (partitioned path at this size) equals an exact host count of the rows
+    assert raw.unique == len(np.unique(raw.panels, axis=0))
     # spot-check three windows of the stream against the oracle
     o = oracle_read(*inst_paths("sf_e_110"), k)
     for begin in (0, 500000, S - 2000):
@@ -273,3 +275,27 @@ def test_hash_buckets(gpu_available, world):
         want = h.view(np.uint64)[owner == np.uint64(w)]
         assert sorted(map(tuple, seg.tolist())) == sorted(map(tuple, want.tolist()))
         start += c[w]
+
+
+@pytest.mark.parametrize("name,k,S", [("couples_panel_from_twenty_people_no_constraints_2", 2, 300000),
+                                      ("example_small_20", 20, 200000), ("sf_e_110", 110, 100000),
+                                      ("rejecty_6", 6, 400000)])
+def test_unique_partitioned_matches_oracle(gpu_available, name, k, S):
+    """csa_unique_async at sizes that take the partitioned path (duplicate-heavy couples / rejecty:
+    a few hundred distinct panels; sf_e: all distinct) == the C oracle's exact count, and == the
+    single-table path (CSA_UNIQUE_PART=0)."""
+    import os
+    A = pkg("analysis")
+    inst, enc = _enc(name, k)
+    o = oracle_read(*inst_paths(name), k)
+    rc, opanels, _, _ = coracle.draw(o, k, 13, 0, S)
+    assert rc == 0
+    want = coracle.unique(opanels, o.n)
+    got = {}
+    for mode in ("1", "0"):
+        os.environ["CSA_UNIQUE_PART"] = mode
+        try:
+            got[mode] = A.legacy_sample_raw(enc, k, S, 13, want_pairs=False, want_panels=False).unique
+        finally:
+            os.environ.pop("CSA_UNIQUE_PART", None)
+    assert got["1"] == got["0"] == want
