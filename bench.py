@@ -176,7 +176,8 @@ def main():
         if evs:
             evs[5].record(stream)
         if world > 1:
-            last["unique"] = Dd.combine(pipe.counts, pipe.pairs, pipe.hashes[: 2 * S], table=table, stream=stream)[2]
+            last["unique"] = Dd.combine(pipe.counts, pipe.pairs, pipe.hashes[: 2 * S], table=table, stream=stream,
+                                        pair_bound=S * world)[2]
         if evs:
             evs[6].record(stream)
             ev_log.append(evs)
@@ -266,7 +267,7 @@ def main():
     # results of the last step (whole job): a rehearsal of --gpus N --panels P must match a single-GPU
     # run with --panels N*P (same global panel indices)
     checks = {"last_step_unique": int(last["unique"].item()), "last_step_count_sum": int(pipe.counts.sum().item()),
-              "last_step_pair_sum": int(pipe.pairs.sum().item()) if want_pairs else None}
+              "last_step_pair_sum": int(torch.triu(pipe.pairs.view(enc.n, enc.n)).sum().item()) if want_pairs else None}
     total = S * world * args.steps
     result = {
         "metric": "LEGACY panels/sec (node) at sf_e_110 shape; XtX MFMA util; speedup vs CPU",

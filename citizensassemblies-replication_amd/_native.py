@@ -60,6 +60,8 @@ SIGNATURES = {
     "csa_unique_hashes_async": (ctypes.c_int, [_P, _U64, _U32, _U32, _P, _U64, _P, _P]),
     "csa_pair_histogram_async": (ctypes.c_int, [_P, _I32, _P, _U64, _P, _P]),
     "csa_hash_buckets_async": (ctypes.c_int, [_P, _U64, _U32, _P, _P, _P, _P]),
+    "csa_pairs_pack_async": (ctypes.c_int, [_P, _I32, _P, _P]),
+    "csa_pairs_unpack_async": (ctypes.c_int, [_P, _I32, _P, _P]),
     "csa_status_decode": (ctypes.c_int, [_P]),
 }
 

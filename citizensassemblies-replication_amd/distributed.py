@@ -8,7 +8,9 @@ is needed for the draw itself.
 
 Exchange steps (the only collectives on the path):
   * per-person counts  all_reduce(SUM) int64[n]
-  * pair counts        all_reduce(SUM) int64[n*n]   (upper triangle meaningful)
+  * pair counts        all_reduce(SUM) of the upper triangle packed to int32
+                       (csa_pairs_pack/unpack_async; int64[n*n] if a count may
+                       reach 2^31)
   * distinct panels    every 128-bit panel hash goes to its OWNER rank
                        (h1 % world) with one all_to_all (buckets from
                        csa_hash_buckets_async); the owner counts its distinct
@@ -145,7 +147,28 @@ def exchange_hashes(hashes, stream=None):
     return recv.to(hashes.device) if via_host else recv
 
 
-def combine(counts, pairs, hashes, table=None, stream=None):
+def _all_reduce_pairs(pairs, pair_bound, stream):
+    """all_reduce(SUM) of the pair counts.  On GPU tensors with every summed count < 2^31
+    (``pair_bound``: the panels of the whole job) only the upper triangle travels, as int32."""
+    import torch
+    import torch.distributed as dist
+    n = int(round(pairs.numel() ** 0.5))
+    if pairs.is_cuda and pair_bound is not None and pair_bound < 2 ** 31 and not _host_collectives(pairs):
+        from . import _native as N
+        sp = ctypes.c_void_p((stream or torch.cuda.current_stream(pairs.device)).cuda_stream)
+        packed = torch.empty(n * (n + 1) // 2, dtype=torch.int32, device=pairs.device)
+        N.check(N.lib().csa_pairs_pack_async(N.ptr(pairs), n, N.ptr(packed), sp))
+        dist.all_reduce(packed, op=dist.ReduceOp.SUM)
+        N.check(N.lib().csa_pairs_unpack_async(N.ptr(packed), n, N.ptr(pairs), sp))
+    elif _host_collectives(pairs):
+        h = pairs.cpu()
+        dist.all_reduce(h, op=dist.ReduceOp.SUM)
+        pairs.copy_(h)
+    else:
+        dist.all_reduce(pairs, op=dist.ReduceOp.SUM)
+
+
+def combine(counts, pairs, hashes, table=None, stream=None, pair_bound=None):
     """Exchange steps for this rank; returns (counts, pairs, unique_tensor).
 
     counts int64[n], pairs int64[n*n] or None, hashes int64[2*S_local] (this rank's
@@ -155,15 +178,14 @@ def combine(counts, pairs, hashes, table=None, stream=None):
     """
     import torch
     import torch.distributed as dist
-    for t in (counts, pairs):
-        if t is None:
-            continue
-        if _host_collectives(t):
-            h = t.cpu()
-            dist.all_reduce(h, op=dist.ReduceOp.SUM)
-            t.copy_(h)
-        else:
-            dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    if _host_collectives(counts):
+        h = counts.cpu()
+        dist.all_reduce(h, op=dist.ReduceOp.SUM)
+        counts.copy_(h)
+    else:
+        dist.all_reduce(counts, op=dist.ReduceOp.SUM)
+    if pairs is not None:
+        _all_reduce_pairs(pairs, pair_bound, stream)
     mine = exchange_hashes(hashes, stream)
     if mine.is_cuda:
         from . import _native as N
@@ -207,6 +229,6 @@ def legacy_probabilities_distributed(instance, iterations, random_seed, keep_pan
     if local:
         pipe.run(random_seed, begin, local)
     pipe.check_status()
-    counts, pairs, u = combine(pipe.counts, pipe.pairs, pipe.hashes[: 2 * local])
+    counts, pairs, u = combine(pipe.counts, pipe.pairs, pipe.hashes[: 2 * local], pair_bound=S)
     raw = A.LegacyRaw(counts.cpu().numpy(), pairs.cpu().numpy().reshape(enc.n, enc.n), int(u.item()), None, None)
     return A.finish(instance, enc, raw, S)

@@ -208,6 +208,12 @@ int csa_pair_histogram_async(const int64_t *d_pairs, int32_t n, uint64_t *d_hist
 int csa_hash_buckets_async(const uint64_t *d_hashes, uint64_t n_hashes, uint32_t world, uint64_t *d_out,
                            uint64_t *d_counts, uint64_t *d_cursor, void *stream);
 
+/* Multi-GPU pair exchange: pack the upper triangle incl. the diagonal of the
+ * n*n int64 pair counts row-major into n(n+1)/2 int32 (every count must be
+ * < 2^31), and unpack it back (overwriting the upper triangle). */
+int csa_pairs_pack_async(const int64_t *d_pairs, int32_t n, int32_t *d_packed, void *stream);
+int csa_pairs_unpack_async(const int32_t *d_packed, int32_t n, int64_t *d_pairs, void *stream);
+
 /* Decode a device status block (host copy of the 4 words) into a CSA_* code
  * and set csa_last_error() accordingly. */
 int csa_status_decode(const uint32_t *h_status);

@@ -277,6 +277,63 @@ def test_hash_buckets(gpu_available, world):
         start += c[w]
 
 
+@pytest.mark.parametrize("n", [1, 7, 110, 257, 1727])
+def test_pairs_pack_roundtrip(gpu_available, n):
+    """csa_pairs_pack/unpack_async: the upper triangle (incl. diagonal) packed row-major into int32
+    and written back; the strict lower triangle is left untouched."""
+    import torch
+    N = pkg("_native")
+    rng = np.random.default_rng(n)
+    m = rng.integers(0, 2 ** 31 - 1, size=(n, n), dtype=np.int64)
+    d = torch.from_numpy(m.reshape(-1)).cuda()
+    packed = torch.empty(n * (n + 1) // 2, dtype=torch.int32, device="cuda")
+    N.check(N.lib().csa_pairs_pack_async(N.ptr(d), n, N.ptr(packed), None))
+    torch.cuda.synchronize()
+    iu = np.triu_indices(n)
+    assert np.array_equal(packed.cpu().numpy().astype(np.int64), m[iu])
+    packed.mul_(2)
+    lower = np.tril_indices(n, -1)
+    N.check(N.lib().csa_pairs_unpack_async(N.ptr(packed), n, N.ptr(d), None))
+    torch.cuda.synchronize()
+    back = d.cpu().numpy().reshape(n, n)
+    assert np.array_equal(back[iu], (2 * m[iu]).astype(np.int32).astype(np.int64))
+    assert np.array_equal(back[lower], m[lower])
+
+
+def test_combine_rccl_world1(gpu_available):
+    """distributed.combine over a one-rank RCCL group on the GPU: the packed int32 pair all-reduce,
+    the count all-reduce and the hash all-to-all leave the single-GPU results unchanged."""
+    import socket
+    import torch
+    import torch.distributed as dist
+    A = pkg("analysis")
+    Dd = pkg("distributed")
+    Dv = pkg("device")
+    inst, enc = _enc("sf_e_110", 110)
+    S = 20000
+    pipe = Dv.DevicePipeline(enc, 110, S)
+    pipe.reset()
+    pipe.run(5, 0, S)
+    pipe.check_status()
+    want_counts = pipe.counts.cpu().numpy().copy()
+    want_pairs = pipe.pairs.cpu().numpy().reshape(enc.n, enc.n).copy()
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    dist.init_process_group("nccl", init_method="tcp://127.0.0.1:%d" % port, rank=0, world_size=1)
+    try:
+        counts, pairs, u = Dd.combine(pipe.counts, pipe.pairs, pipe.hashes[: 2 * S], stream=pipe.stream,
+                                      pair_bound=S)
+        torch.cuda.synchronize()
+        got_pairs = pairs.cpu().numpy().reshape(enc.n, enc.n)
+    finally:
+        dist.destroy_process_group()
+    assert np.array_equal(counts.cpu().numpy(), want_counts)
+    iu = np.triu_indices(enc.n)
+    assert np.array_equal(got_pairs[iu], want_pairs[iu])
+    assert int(u.item()) == S      # sf_e_110 at 2e4 panels: all distinct
+
+
 @pytest.mark.parametrize("name,k,S", [("couples_panel_from_twenty_people_no_constraints_2", 2, 300000),
                                       ("example_small_20", 20, 200000), ("sf_e_110", 110, 100000),
                                       ("rejecty_6", 6, 400000)])
