@@ -10,7 +10,7 @@ import subprocess
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(HERE)
-LIB_PATH = os.path.join(HERE, "libcsa_legacy.so")
+LIB_PATH = os.environ.get("CSA_LIB") or os.path.join(HERE, "libcsa_legacy.so")  # CSA_LIB: A/B builds
 SRC = os.path.join(HERE, "csrc", "csa_legacy.hip")
 HEADER = os.path.join(REPO, "include", "csa_legacy.h")
 

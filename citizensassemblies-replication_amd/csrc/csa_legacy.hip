@@ -1261,6 +1261,7 @@ struct csa_instance {
     uint32_t *d_pmask = nullptr;  // n person feature masks (F <= 32 only)
     int32_t max_abs = 0;  // max |fmin| / |sel0| bound for the cross-multiplication range check
     bool zero_max_min = false;  // some feature has max 0 and min > 0 (draw_batch_kernel excludes it)
+    bool sel_over_max = false;  // some feature starts with selected > max (draw_lane_kernel excludes it)
     // grow-only device scratch + a stream for the repeated small host-API calls
     // (csa_first_panel_not_in: XMIN calls it 5n times)
     void *scratch[8] = {};
@@ -1413,7 +1414,9 @@ int pick_draw_config(const csa_instance *I, bool general, DrawConfig &c) {
     if (const char *e = getenv("CSA_DRAW_GROUP")) lane_g = atoi(e) == 1 ? 1 : 0;
     if (const char *e = getenv("CSA_DRAW_LANE")) lane_g = atoi(e);
     // the lane kernel packs need and remaining as 16-bit halves: |min|, |selected| < 2^15 (n <= 16384)
-    if (!general && small && I->W <= 32 && I->max_abs < 32768 && (lane_g == 1 || lane_g == 2 || lane_g == 4)) {
+    // and tests "selected == max" as need <= min - max (selected never starts above max)
+    if (!general && small && I->W <= 32 && I->max_abs < 32768 && !I->sel_over_max &&
+        (lane_g == 1 || lane_g == 2 || lane_g == 4)) {
         // draw_lane_kernel: FN in {8, 16, 32} (FN / G >= 4), WN in {4, 8, 16, 28, 32}
         c.G = lane_g;
         c.lane = true;
@@ -1665,8 +1668,12 @@ int csa_instance_set_state(csa_instance *I, const int32_t *sel, const int32_t *r
     for (int p = 0; p < I->n; ++p) all[p >> 6] |= 1ull << (p & 63);
     int32_t mx = 0;
     for (int f = 0; f < I->F; ++f) mx = std::max(mx, std::abs(I->fmin[f]));
+    I->sel_over_max = false;
     if (sel)
-        for (int f = 0; f < I->F; ++f) mx = std::max(mx, std::abs(sel[f]));
+        for (int f = 0; f < I->F; ++f) {
+            mx = std::max(mx, std::abs(sel[f]));
+            if (sel[f] > I->fmax[f]) I->sel_over_max = true;
+        }
     I->max_abs = mx;
     if (present)
         for (int w = 0; w < I->W; ++w)
