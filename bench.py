@@ -2,9 +2,12 @@
 
 One "step" = one pass of the hot path (analysis.py:162-191) over one batch of
 synthetic-instance panels per GPU, entirely on the device:
-draw (with restarts) -> per-person counts -> pair counts X^T X (int8 MFMA) ->
-distinct-panel count, plus (N > 1) the RCCL exchange (all_reduce of counts and
-pairs, all_gather of panel hashes + device owner dedupe + all_reduce).
+draw (with restarts) -> panel hashes -> per-person counts -> pair counts X^T X
+(fp4 MFMA) -> distinct-panel count, plus (N > 1) the RCCL exchange (all_reduce of
+counts and packed pairs, all_to_all of panel hashes to their owner rank + device
+dedupe + all_reduce).  By default step i+1's draw runs on a second stream while
+step i is counted (as csa_legacy_sample pipelines its chunks); --no-overlap
+serialises them.
 
     python bench.py [--gpus N --steps K --warmup W] [--config sf_e_110] [--panels P]
 
@@ -54,6 +57,9 @@ def parse():
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--no-pairs", action="store_true")
     ap.add_argument("--pair-engine", default="fp4", choices=sorted(PAIR_ENGINES))
+    ap.add_argument("--no-overlap", action="store_true",
+                    help="run each step's draw after the previous step's counting (default: the draw of step "
+                         "i+1 runs on a second stream, into a second panel buffer, while step i is counted)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample duration")
     return ap.parse_args()
@@ -152,15 +158,34 @@ def main():
     ev_log = []
     last = {"unique": pipe.unique}
 
+    # --overlap (default): step i+1's draw (draw_stream, panel buffer (i+1) % 2) runs while step i is
+    # hashed / counted / paired / exchanged on `stream`; every step still does all of its work and
+    # the timed region still ends with a device-wide synchronize
+    overlap = not args.no_overlap
+    draw_stream = torch.cuda.Stream(dev) if overlap else stream
+    bufs = [pipe.panels, torch.empty_like(pipe.panels)] if overlap else [pipe.panels]
+    drawn = [torch.cuda.Event() for _ in bufs]       # draw of the buffer finished (draw_stream)
+    counted = [torch.cuda.Event() for _ in bufs]     # counting of the buffer finished (stream)
+    with torch.cuda.stream(stream):
+        pipe.status.zero_()
+
     def step(i, record):
         begin = (i * world + rank) * S            # global panel indices, distinct per step and rank
-        evs = [torch.cuda.Event(enable_timing=True) for _ in range(len(stages) + 1)] if record else None
-        pipe.reset()
+        evs = [torch.cuda.Event(enable_timing=True) for _ in range(len(stages) + 2)] if record else None
+        b = i % len(bufs)
+        pipe.panels = bufs[b]
+        if overlap:
+            draw_stream.wait_event(counted[b])    # step i-2 is done reading this buffer
+        if evs:
+            evs[-1].record(draw_stream)
+        pipe.draw(args.seed, begin, S, stream=draw_stream)
+        if evs:
+            evs[1].record(draw_stream)
+        drawn[b].record(draw_stream)
+        stream.wait_event(drawn[b])
+        pipe.reset(status=False)
         if evs:
             evs[0].record(stream)
-        pipe.draw(args.seed, begin, S)
-        if evs:
-            evs[1].record(stream)
         pipe.hash(S)
         if evs:
             evs[2].record(stream)
@@ -181,6 +206,7 @@ def main():
         if evs:
             evs[6].record(stream)
             ev_log.append(evs)
+        counted[b].record(stream)
 
     for i in range(args.warmup):
         step(i, False)
@@ -207,7 +233,8 @@ def main():
     stage_ms = {s: 0.0 for s in stages}
     for evs in ev_log:
         for j, s in enumerate(stages):
-            stage_ms[s] += evs[j].elapsed_time(evs[j + 1]) / len(ev_log)
+            a = evs[-1] if s == "draw" else evs[j] if s != "hash" else evs[0]
+            stage_ms[s] += a.elapsed_time(evs[j + 1]) / len(ev_log)
     n, W = enc.n, enc.W
     npad = pipe.npad
     nblk = (S + 63) // 64
@@ -284,7 +311,9 @@ def main():
         "data": "synthetic instance %s (tests/golden/instances), Philox seed %d" % (inst_dir, args.seed),
         "config": {"workload": "%s: %d LEGACY panels/GPU/step, k=%d, n=%d, C=%d, F=%d, counts+%sunique" % (
             args.config, S, k, n, enc.C, enc.F, "pairs+" if want_pairs else ""),
-            "panels_per_gpu_per_step": S, "instance": inst_dir, "parallelism": "panel shards x%d" % world},
+            "panels_per_gpu_per_step": S, "instance": inst_dir, "parallelism": "panel shards x%d" % world,
+            "pipeline": ("2 streams: step i+1 drawn while step i is hashed/counted/paired%s" % (
+                "/exchanged" if world > 1 else "")) if overlap else "serial"},
         "roofline": roof,
         "kernels": kernels,
         "checks": checks,

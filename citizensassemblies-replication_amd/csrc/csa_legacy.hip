@@ -1512,6 +1512,9 @@ int read_status(const uint32_t *d_status, hipStream_t stream, uint32_t *h) {
     return CSA_OK;
 }
 
+// csa_legacy_sample's pipeline chunk (panels): 2^20 = one bench step at sf_e
+constexpr uint64_t kSampleChunk = 1ull << 20;
+
 uint64_t pow2_at_least(uint64_t x) {
     uint64_t p = 1;
     while (p < x) p <<= 1;
@@ -1991,54 +1994,81 @@ int csa_legacy_sample(csa_instance *I, int32_t k, uint64_t seed, uint64_t panel_
     ScopedDevice sd(I->device);
     const int n = I->n, W = I->W;
     const int npad = csa_xt_pad(std::max(n, 1));
-    const uint64_t nblk = (n_panels + 63) / 64;
-    hipStream_t st = nullptr;
-    HIPCHK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
-    struct StreamGuard {
-        hipStream_t s;
-        ~StreamGuard() { (void)hipStreamDestroy(s); }
-    } sg{st};
-    DevBuf<uint64_t> panels, hashes, xt, table, uniq;
+    // Chunked two-stream pipeline: chunk c + 1 is drawn (stream sd) while chunk c is hashed,
+    // transposed, counted and paired (stream sp); the panels and hashes buffers hold the whole
+    // batch (output copy, exact distinct count at the end), XT and the pair scratch one chunk.
+    uint64_t chunk = kSampleChunk;
+    if (const char *e = getenv("CSA_SAMPLE_CHUNK")) chunk = std::max<uint64_t>(64, strtoull(e, nullptr, 10));
+    chunk = std::min(chunk, std::max<uint64_t>(n_panels, 1));
+    const uint64_t cblk = (chunk + 63) / 64;
+    DevBuf<uint64_t> panels, hashes, xt, table, uniq;  // freed after the guard below drained the streams
     DevBuf<int64_t> counts, pairs;
     DevBuf<uint32_t> attempts, status;
+    DevBuf<int32_t> scratch;
+    hipStream_t sdraw = nullptr, spost = nullptr;
+    hipEvent_t drawn = nullptr;
+    struct Guard {
+        hipStream_t a = nullptr, b = nullptr;
+        hipEvent_t e = nullptr;
+        ~Guard() {  // drain both streams before the buffers below are freed
+            if (a) (void)hipStreamSynchronize(a);
+            if (b) (void)hipStreamSynchronize(b);
+            if (e) (void)hipEventDestroy(e);
+            if (a) (void)hipStreamDestroy(a);
+            if (b) (void)hipStreamDestroy(b);
+        }
+    } guard;
+    HIPCHK(hipStreamCreateWithFlags(&sdraw, hipStreamNonBlocking));
+    guard.a = sdraw;
+    HIPCHK(hipStreamCreateWithFlags(&spost, hipStreamNonBlocking));
+    guard.b = spost;
+    HIPCHK(hipEventCreateWithFlags(&drawn, hipEventDisableTiming));
+    guard.e = drawn;
     int rc;
     const bool want_unique = flags & CSA_WANT_UNIQUE, want_pairs = flags & CSA_WANT_PAIRS;
     const bool want_counts = flags & CSA_WANT_COUNTS;
     const uint64_t slots = pow2_at_least(std::max<uint64_t>(2 * n_panels, 64));
-    if ((rc = dalloc(&panels.p, n_panels * W)) || (rc = dalloc(&status.p, 4))) return rc;
-    if (want_unique && ((rc = dalloc(&hashes.p, 2 * n_panels)) || (rc = dalloc(&table.p, slots)) ||
-                        (rc = dalloc(&uniq.p, 1))))
+    const uint64_t sb = want_pairs ? csa_pair_scratch_bytes(n, cblk, CSA_PAIR_FP4) : 0;
+    if ((rc = dalloc(&panels.p, std::max<uint64_t>(n_panels, 1) * W)) || (rc = dalloc(&status.p, 4))) return rc;
+    if (want_unique && ((rc = dalloc(&hashes.p, 2 * std::max<uint64_t>(n_panels, 1))) ||
+                        (rc = dalloc(&table.p, slots)) || (rc = dalloc(&uniq.p, 1))))
         return rc;
-    if (attempts_out && (rc = dalloc(&attempts.p, n_panels))) return rc;
+    if (attempts_out && (rc = dalloc(&attempts.p, std::max<uint64_t>(n_panels, 1)))) return rc;
     if ((want_counts || want_pairs) && (rc = dalloc(&counts.p, n))) return rc;
-    if (want_pairs && ((rc = dalloc(&xt.p, nblk * npad)) || (rc = dalloc(&pairs.p, (size_t)n * n)))) return rc;
-    HIPCHK(hipMemsetAsync(status.p, 0, 16, st));
-    if (counts.p) HIPCHK(hipMemsetAsync(counts.p, 0, (size_t)n * 8, st));
-    if (pairs.p) HIPCHK(hipMemsetAsync(pairs.p, 0, (size_t)n * n * 8, st));
-    if (uniq.p) HIPCHK(hipMemsetAsync(uniq.p, 0, 8, st));
-    if ((rc = launch_draw(I, k, seed, panel_begin, n_panels, max_attempts, 0, 0, panels.p, hashes.p, attempts.p,
-                          nullptr, status.p, nullptr, nullptr, nullptr, st)))
+    if (want_pairs && ((rc = dalloc(&xt.p, cblk * npad)) || (rc = dalloc(&pairs.p, (size_t)n * n)) ||
+                       (rc = dalloc(&scratch.p, sb / sizeof(int32_t) + 1))))
         return rc;
-    uint32_t hs[4];
-    if ((rc = read_status(status.p, st, hs))) return rc;
-    if ((rc = csa_status_decode(hs))) return rc;
-    if (counts.p && (rc = csa_transpose_count_async(panels.p, n_panels, n, xt.p, counts.p, st))) return rc;
-    if (pairs.p) {
-        DevBuf<int32_t> scratch;
-        const uint64_t sb = csa_pair_scratch_bytes(n, nblk, CSA_PAIR_FP4);
-        if ((rc = dalloc(&scratch.p, sb / sizeof(int32_t)))) return rc;
-        if ((rc = csa_pair_counts_ex_async(xt.p, nblk, n, pairs.p, CSA_PAIR_FP4, scratch.p, sb, st))) return rc;
-        HIPCHK(hipStreamSynchronize(st));  // scratch is freed at scope exit
+    HIPCHK(hipMemsetAsync(status.p, 0, 16, sdraw));
+    if (counts.p) HIPCHK(hipMemsetAsync(counts.p, 0, (size_t)n * 8, spost));
+    if (pairs.p) HIPCHK(hipMemsetAsync(pairs.p, 0, (size_t)n * n * 8, spost));
+    if (uniq.p) HIPCHK(hipMemsetAsync(uniq.p, 0, 8, spost));
+    for (uint64_t off = 0; off < n_panels; off += chunk) {
+        const uint64_t len = std::min(chunk, n_panels - off);
+        uint64_t *cp = panels.p + off * W;
+        if ((rc = launch_draw(I, k, seed, panel_begin + off, len, max_attempts, 0, 0, cp, nullptr,
+                              attempts.p ? attempts.p + off : nullptr, nullptr, status.p, nullptr, nullptr,
+                              nullptr, sdraw)))
+            return rc;
+        HIPCHK(hipEventRecord(drawn, sdraw));
+        HIPCHK(hipStreamWaitEvent(spost, drawn, 0));
+        if (want_unique && (rc = csa_panel_hash_async(cp, len, W, hashes.p + 2 * off, spost))) return rc;
+        if (counts.p && (rc = csa_transpose_count_async(cp, len, n, xt.p, counts.p, spost))) return rc;
+        if (pairs.p && (rc = csa_pair_counts_ex_async(xt.p, (len + 63) / 64, n, pairs.p, CSA_PAIR_FP4, scratch.p,
+                                                      sb, spost)))
+            return rc;
     }
-    if (want_unique && (rc = csa_unique_async(hashes.p, panels.p, n_panels, W, table.p, slots, uniq.p, st)))
+    uint32_t hs[4];
+    if ((rc = read_status(status.p, sdraw, hs))) return rc;
+    if ((rc = csa_status_decode(hs))) return rc;
+    if (want_unique && (rc = csa_unique_async(hashes.p, panels.p, n_panels, W, table.p, slots, uniq.p, spost)))
         return rc;
     if (flags & CSA_WANT_PANELS)
-        HIPCHK(hipMemcpyAsync(panels_out, panels.p, n_panels * W * 8, hipMemcpyDeviceToHost, st));
-    if (want_counts) HIPCHK(hipMemcpyAsync(person_counts, counts.p, (size_t)n * 8, hipMemcpyDeviceToHost, st));
-    if (want_pairs) HIPCHK(hipMemcpyAsync(pair_counts, pairs.p, (size_t)n * n * 8, hipMemcpyDeviceToHost, st));
-    if (want_unique) HIPCHK(hipMemcpyAsync(unique_out, uniq.p, 8, hipMemcpyDeviceToHost, st));
-    if (attempts_out) HIPCHK(hipMemcpyAsync(attempts_out, attempts.p, n_panels * 4, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipStreamSynchronize(st));
+        HIPCHK(hipMemcpyAsync(panels_out, panels.p, n_panels * W * 8, hipMemcpyDeviceToHost, spost));
+    if (want_counts) HIPCHK(hipMemcpyAsync(person_counts, counts.p, (size_t)n * 8, hipMemcpyDeviceToHost, spost));
+    if (want_pairs) HIPCHK(hipMemcpyAsync(pair_counts, pairs.p, (size_t)n * n * 8, hipMemcpyDeviceToHost, spost));
+    if (want_unique) HIPCHK(hipMemcpyAsync(unique_out, uniq.p, 8, hipMemcpyDeviceToHost, spost));
+    if (attempts_out) HIPCHK(hipMemcpyAsync(attempts_out, attempts.p, n_panels * 4, hipMemcpyDeviceToHost, spost));
+    HIPCHK(hipStreamSynchronize(spost));
     return CSA_OK;
 }
 

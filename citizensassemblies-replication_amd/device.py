@@ -61,21 +61,25 @@ class DevicePipeline:
             self.unique = torch.zeros(1, dtype=torch.int64, device=dev)
         _ = enc.handle  # upload the instance on this device
 
-    def reset(self):
+    def reset(self, status=True):
         with torch.cuda.stream(self.stream):
-            self.status.zero_()
+            if status:
+                self.status.zero_()
             self.counts.zero_()
             self.unique.zero_()
             if self.pairs is not None:
                 self.pairs.zero_()
 
     # individual stages (stream-ordered, no sync) -------------------------------------------
-    def draw(self, seed, panel_begin, S, max_attempts=0):
-        assert S <= self.max_panels
+    def draw(self, seed, panel_begin, S, max_attempts=0, stream=None):
+        """Draw into self.panels on ``stream`` (default: the pipeline's stream).  A caller that
+        overlaps the draw of the next batch with this batch's counting swaps ``self.panels``
+        between two buffers and orders the streams with events (bench.py --overlap)."""
+        assert S <= self.max_panels and self.panels.numel() >= S * self.enc.W
         N.check(N.lib().csa_draw_async(self.enc.handle, self.k, int(seed) & 0xFFFFFFFFFFFFFFFF, int(panel_begin),
                                        int(S), max_attempts, N.ptr(self.panels), None,
                                        N.ptr(self.attempts), None, N.ptr(self.status),
-                                       _stream_ptr(self.stream)))
+                                       _stream_ptr(stream or self.stream)))
 
     def hash(self, S):
         N.check(N.lib().csa_panel_hash_async(N.ptr(self.panels), int(S), self.enc.W, N.ptr(self.hashes),

@@ -45,6 +45,24 @@ def test_sample_matches_reference_golden(gpu_available, case):
     assert _sha(up / g["S"]) == g["pair_prob_sha256"]        # the reference's float64 pair values
 
 
+@pytest.mark.parametrize("case", PHILOX_CASES)
+@pytest.mark.parametrize("chunk", [64, 1000])
+def test_sample_chunked_pipeline_matches_golden(gpu_available, case, chunk, monkeypatch):
+    """csa_legacy_sample's two-stream chunk pipeline (draw chunk c+1 while chunk c is counted) with
+    small chunks, including ones that are not a multiple of 64 panels: identical to the goldens."""
+    monkeypatch.setenv("CSA_SAMPLE_CHUNK", str(chunk))
+    A = pkg("analysis")
+    g = golden(case)
+    inst, enc = _enc(g["instance"], g["k"])
+    raw = A.legacy_sample_raw(enc, g["k"], g["S"], g["seed"], want_pairs=True, want_panels=True,
+                              want_attempts=True)
+    assert _sha(raw.panels) == g["panels_sha256"]
+    assert raw.attempts.tolist() == g["attempts"]
+    assert raw.counts.tolist() == g["counts"]
+    assert raw.unique == g["unique"]
+    assert _sha(raw.pairs[np.triu_indices(enc.n, 1)]) == g["pair_upper_sha256"]
+
+
 @pytest.mark.parametrize("case", ["couples_s0", "example_small_20_s0", "sf_e_tight_110_s1", "pathological_5_s0"])
 def test_legacy_find_pick_order(gpu_available, case):
     A = pkg("analysis")
