@@ -60,6 +60,8 @@ def parse():
     ap.add_argument("--no-overlap", action="store_true",
                     help="run each step's draw after the previous step's counting (default: the draw of step "
                          "i+1 runs on a second stream, into a second panel buffer, while step i is counted)")
+    ap.add_argument("--iso-steps", type=int, default=2,
+                    help="serial steps after the timed region that measure each kernel alone (not in `value`)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample duration")
     return ap.parse_args()
@@ -169,19 +171,20 @@ def main():
     with torch.cuda.stream(stream):
         pipe.status.zero_()
 
-    def step(i, record):
+    def step(i, log, ov=overlap):
         begin = (i * world + rank) * S            # global panel indices, distinct per step and rank
-        evs = [torch.cuda.Event(enable_timing=True) for _ in range(len(stages) + 2)] if record else None
-        b = i % len(bufs)
+        evs = [torch.cuda.Event(enable_timing=True) for _ in range(len(stages) + 2)] if log is not None else None
+        b = i % len(bufs) if ov else 0
+        ds = draw_stream if ov else stream
         pipe.panels = bufs[b]
-        if overlap:
-            draw_stream.wait_event(counted[b])    # step i-2 is done reading this buffer
+        if ov:
+            ds.wait_event(counted[b])             # step i-2 is done reading this buffer
         if evs:
-            evs[-1].record(draw_stream)
-        pipe.draw(args.seed, begin, S, stream=draw_stream)
+            evs[-1].record(ds)
+        pipe.draw(args.seed, begin, S, stream=ds)
         if evs:
-            evs[1].record(draw_stream)
-        drawn[b].record(draw_stream)
+            evs[1].record(ds)
+        drawn[b].record(ds)
         stream.wait_event(drawn[b])
         pipe.reset(status=False)
         if evs:
@@ -205,11 +208,11 @@ def main():
                                         pair_bound=S * world)[2]
         if evs:
             evs[6].record(stream)
-            ev_log.append(evs)
+            log.append(evs)
         counted[b].record(stream)
 
     for i in range(args.warmup):
-        step(i, False)
+        step(i, None)
     torch.cuda.synchronize()
     pipe.check_status()
     if world > 1:
@@ -217,7 +220,7 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
-        step(args.warmup + i, True)
+        step(args.warmup + i, ev_log)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -229,12 +232,32 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    # per-stage device time (ms) averaged over the timed steps
-    stage_ms = {s: 0.0 for s in stages}
-    for evs in ev_log:
-        for j, s in enumerate(stages):
-            a = evs[-1] if s == "draw" else evs[j] if s != "hash" else evs[0]
-            stage_ms[s] += a.elapsed_time(evs[j + 1]) / len(ev_log)
+    # results of the last timed step (whole job): a rehearsal of --gpus N --panels P must match a
+    # single-GPU run with --panels N*P (same global panel indices)
+    checks = {"last_step_unique": int(last["unique"].item()), "last_step_count_sum": int(pipe.counts.sum().item()),
+              "last_step_pair_sum": int(torch.triu(pipe.pairs.view(enc.n, enc.n)).sum().item()) if want_pairs else None}
+
+    def stage_times(log):
+        """per-stage device time (ms) averaged over the logged steps (HIP events on the launch streams)"""
+        out = {s: 0.0 for s in stages}
+        for evs in log:
+            for j, s in enumerate(stages):
+                a = evs[-1] if s == "draw" else evs[j] if s != "hash" else evs[0]
+                out[s] += a.elapsed_time(evs[j + 1]) / len(log)
+        return out
+
+    # stage times inside the timed region; with the two-stream pipeline the counting kernels share
+    # the CUs with the next step's draw, so their durations there are inflated.  A short serial pass
+    # AFTER the timed region (not part of `value`) measures every kernel alone on the device.
+    stage_pipe = stage_times(ev_log)
+    iso_log = []
+    if overlap:
+        torch.cuda.synchronize()
+        for i in range(args.iso_steps):
+            step(args.warmup + args.steps + i, iso_log, ov=False)
+        torch.cuda.synchronize()
+        pipe.check_status()
+    stage_ms = stage_times(iso_log) if iso_log else stage_pipe
     n, W = enc.n, enc.W
     npad = pipe.npad
     nblk = (S + 63) // 64
@@ -267,17 +290,26 @@ def main():
                                          "ms includes the partial-block reduce kernel"}
     if world > 1:
         kernels["exchange"] = {"ms": stage_ms["exchange"]}
-    dominant = max(("draw", "hash", "xt_count", "pairs", "unique"), key=lambda s: stage_ms[s])
+    for key, st in (("draw", "draw"), ("hash", "hash"), ("xt_count", "xt_count"), ("unique", "unique"),
+                    ("pairs_mfma", "pairs"), ("exchange", "exchange")):
+        if key in kernels:
+            kernels[key]["ms_in_timed_region"] = stage_pipe[st]
+    kernel_timing = ("'ms' = each kernel alone (serial pass of %d steps after the timed region); "
+                         "'ms_in_timed_region' = HIP events on the launch streams inside the timed region, "
+                         "where the counting kernels share the CUs with the next step's draw" % len(iso_log)
+                         ) if iso_log else "HIP events on the launch stream inside the timed region (serial steps)"
+    dominant = max(("draw", "hash", "xt_count", "pairs", "unique"), key=lambda s: stage_pipe[s])
     pmc = load_pmc_traffic(args.config)
+    # the roofline's kernel duration is the one inside the timed region (what rocprofv3 averages)
     if dominant == "pairs":
-        ach = pair_ops / (stage_ms["pairs"] * 1e-3) / 1e12
+        ach = pair_ops / (stage_pipe["pairs"] * 1e-3) / 1e12
         roof = {"kernel": "pair_mfma_kernel", "bound": "mfma", "achieved": ach, "peak": engine_peak / 1e12,
                 "unit": "TFLOP/s", "frac": ach * 1e12 / engine_peak, "traffic": None}
     else:
         name = {"draw": draw_name, "hash": "panel_hash_kernel", "xt_count": "xt_count_kernel",
                 "unique": "unique_kernel"}[dominant]
         b = {"draw": draw_bytes, "hash": hash_bytes, "xt_count": xt_bytes, "unique": uniq_bytes}[dominant]
-        ach = gbs(b, stage_ms[dominant])
+        ach = gbs(b, stage_pipe[dominant])
         traffic = None
         pk = (pmc or {}).get("per_kernel", {}).get(name)
         if pk and pmc.get("panels") == S:
@@ -291,10 +323,6 @@ def main():
                 kernels["draw"]["pmc_issue"] = pmc["draw_issue"]
                 roof["issue_frac"] = pmc["draw_issue"].get("valu_issue_frac")
 
-    # results of the last step (whole job): a rehearsal of --gpus N --panels P must match a single-GPU
-    # run with --panels N*P (same global panel indices)
-    checks = {"last_step_unique": int(last["unique"].item()), "last_step_count_sum": int(pipe.counts.sum().item()),
-              "last_step_pair_sum": int(torch.triu(pipe.pairs.view(enc.n, enc.n)).sum().item()) if want_pairs else None}
     total = S * world * args.steps
     result = {
         "metric": "LEGACY panels/sec (node) at sf_e_110 shape; XtX MFMA util; speedup vs CPU",
@@ -316,6 +344,7 @@ def main():
                 "/exchanged" if world > 1 else "")) if overlap else "serial"},
         "roofline": roof,
         "kernels": kernels,
+        "kernel_timing": kernel_timing,
         "checks": checks,
     }
     if want_pairs:
