@@ -243,9 +243,13 @@ __host__ __device__ inline size_t draw_lds_bytes(int G, int FPL, int WPL, int W,
 // order (legacy_find) and the single-attempt state outputs (find_random_sample_legacy).
 // waves per SIMD requested from the register allocator: small instances fit 6 (80 VGPRs)
 constexpr int draw_occupancy(int FPL, int WPL) { return FPL + WPL <= 4 ? 6 : 1; }
+// threads per workgroup: the LDS feature rows are shared by the workgroup, so large instances
+// (n = 8192: 66 KB of rows + 1.8 KB per group) get 512 threads = 2 waves per SIMD in one
+// workgroup per CU, where 256 threads left 1 wave per SIMD (LDS-limited to one workgroup)
+constexpr int draw_threads(int FPL, int WPL) { return (FPL + WPL > 4 && WPL <= 8) ? 2 * kDrawThreads : kDrawThreads; }
 
 template <int G, int FPL, int WPL, bool GENERAL>
-__global__ __launch_bounds__(kDrawThreads, draw_occupancy(FPL, WPL)) void draw_kernel(DrawArgs A) {
+__global__ __launch_bounds__(draw_threads(FPL, WPL), draw_occupancy(FPL, WPL)) void draw_kernel(DrawArgs A) {
     constexpr int NL = group_levels(G);
     constexpr int FR = G * FPL;        // LDS feature rows
     constexpr int Ls = G * WPL + 1;    // LDS row stride (words)
@@ -1483,7 +1487,7 @@ int launch_draw(const csa_instance *I, int32_t k, uint64_t seed, uint64_t panel_
     A.sel_out = d_sel_out;
     A.rem_out = d_rem_out;
     A.present_out = d_present_out;
-    const int threads = cfg.lane ? kLaneThreads : cfg.batch ? kBatchThreads : kDrawThreads;
+    const int threads = cfg.lane ? kLaneThreads : cfg.batch ? kBatchThreads : draw_threads(cfg.FPL, cfg.WPL);
     const int groups_wg = threads / cfg.G;
     const size_t lds = cfg.lane    ? lane_lds_bytes(cfg.G, cfg.FPL, cfg.WPL, I->n)
                        : cfg.batch ? batch_lds_bytes(cfg.G, cfg.FPL, cfg.WPL, I->n, I->W, k, groups_wg)
