@@ -76,13 +76,21 @@ __device__ __forceinline__ void philox4x32_10(uint32_t &c0, uint32_t &c1, uint32
 
 // position (0..63) of the rr-th (1-based) set bit of m; requires 1 <= rr <= popcount(m)
 __device__ __forceinline__ int select_bit(uint64_t m, int rr) {
+    // the 32-bit half first, then a binary search on 32-bit values (no 64-bit masks or shifts)
+    uint32_t x = (uint32_t)m;
     int pos = 0;
+    const int c0 = __popc(x);
+    if (rr > c0) {
+        rr -= c0;
+        x = (uint32_t)(m >> 32);
+        pos = 32;
+    }
 #pragma unroll
-    for (int s = 32; s >= 1; s >>= 1) {
-        const int c = __popcll(m & ((1ull << s) - 1));
+    for (int s = 16; s >= 1; s >>= 1) {
+        const int c = __popc(x & ((1u << s) - 1u));
         if (rr > c) {
             rr -= c;
-            m >>= s;
+            x >>= s;
             pos += s;
         }
     }
