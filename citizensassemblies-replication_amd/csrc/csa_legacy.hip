@@ -949,7 +949,8 @@ __global__ __launch_bounds__(256, 1) void pair_mfma_wide_kernel(const uint64_t *
 }
 
 __global__ __launch_bounds__(256) void pair_reduce_kernel(const int32_t *__restrict__ part, int n, int nbt,
-                                                          int nsplit, int64_t *__restrict__ pairs) {
+                                                          int nsplit, int64_t *__restrict__ pairs,
+                                                          int overwrite) {
     int bi, bj;
     tri_block((int)blockIdx.y, nbt, bi, bj);
     const int e = blockIdx.x * 256 + threadIdx.x;  // element of the 256 x 256 block
@@ -958,7 +959,10 @@ __global__ __launch_bounds__(256) void pair_reduce_kernel(const int32_t *__restr
     const int32_t *p = part + (size_t)blockIdx.y * nsplit * kPairBlock * kPairBlock + e;
     int64_t acc = 0;
     for (int k = 0; k < nsplit; ++k) acc += p[(size_t)k * kPairBlock * kPairBlock];
-    if (acc) pairs[(size_t)row * n + col] += acc;
+    // overwrite (CSA_PAIR_OVERWRITE): every element of the block is stored, so the caller needs
+    // no zero-fill of the n x n output before a fresh batch
+    if (overwrite) pairs[(size_t)row * n + col] = acc;
+    else if (acc) pairs[(size_t)row * n + col] += acc;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1866,13 +1870,18 @@ int pair_plan(int32_t n, uint64_t n_blocks, uint32_t engine, PairPlan &p) {
 
 uint64_t csa_pair_scratch_bytes(int32_t n, uint64_t n_blocks, uint32_t engine) {
     PairPlan p;
-    if (n <= 0 || n_blocks == 0 || pair_plan(n, n_blocks, engine, p)) return 0;
+    if (n <= 0 || n_blocks == 0 || pair_plan(n, n_blocks, engine & ~CSA_PAIR_OVERWRITE, p)) return 0;
     return (uint64_t)p.ntri * p.nsplit * kPairBlock * kPairBlock * sizeof(int32_t);
 }
 
 int csa_pair_counts_ex_async(const uint64_t *d_xt, uint64_t n_blocks, int32_t n, int64_t *d_pairs,
                              uint32_t engine, void *d_scratch, uint64_t scratch_bytes, void *stream) {
     if (n <= 0 || !d_xt || !d_pairs) return fail(CSA_E_INVALID, "pairs: bad arguments");
+    const bool overwrite = (engine & CSA_PAIR_OVERWRITE) != 0u;
+    engine &= ~CSA_PAIR_OVERWRITE;
+    const hipStream_t st = (hipStream_t)stream;
+    if (overwrite && (n_blocks == 0 || !d_scratch))  // no reduce pass to store every element
+        HIPCHK(hipMemsetAsync(d_pairs, 0, (size_t)n * n * sizeof(int64_t), st));
     if (n_blocks == 0) return CSA_OK;
     PairPlan p;
     int rc = pair_plan(n, n_blocks, engine, p);
@@ -1883,7 +1892,6 @@ int csa_pair_counts_ex_async(const uint64_t *d_xt, uint64_t n_blocks, int32_t n,
                     (unsigned long long)scratch_bytes, (unsigned long long)csa_pair_scratch_bytes(n, n_blocks, engine));
     const dim3 grid(p.ntri * p.nsplit), block(kPairThreads);
     int32_t *part = static_cast<int32_t *>(d_scratch);
-    const hipStream_t st = (hipStream_t)stream;
     // panel blocks staged per barrier (prefetch distance): CSA_PAIR_KB = 4 / 8 / 16 overrides
     int kb = kPairKB;
     if (const char *e = getenv("CSA_PAIR_KB")) kb = atoi(e);
@@ -1915,7 +1923,7 @@ int csa_pair_counts_ex_async(const uint64_t *d_xt, uint64_t n_blocks, int32_t n,
     HIPCHK(hipGetLastError());
     if (partial) {
         hipLaunchKernelGGL(pair_reduce_kernel, dim3(kPairBlock, p.ntri), dim3(256), 0, st, part, n, p.nbt, p.nsplit,
-                           d_pairs);
+                           d_pairs, (int)overwrite);
         HIPCHK(hipGetLastError());
     }
     return CSA_OK;

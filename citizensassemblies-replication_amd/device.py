@@ -61,13 +61,15 @@ class DevicePipeline:
             self.unique = torch.zeros(1, dtype=torch.int64, device=dev)
         _ = enc.handle  # upload the instance on this device
 
-    def reset(self, status=True):
+    def reset(self, status=True, pairs=True):
+        """Zero the accumulators.  ``pairs=False`` skips the n*n pair matrix for a caller whose next
+        ``pair_counts(..., overwrite=True)`` stores the batch's counts instead of adding them."""
         with torch.cuda.stream(self.stream):
             if status:
                 self.status.zero_()
             self.counts.zero_()
             self.unique.zero_()
-            if self.pairs is not None:
+            if pairs and self.pairs is not None:
                 self.pairs.zero_()
 
     # individual stages (stream-ordered, no sync) -------------------------------------------
@@ -95,12 +97,15 @@ class DevicePipeline:
                                                   N.ptr(self.xt) if self.want_pairs else None,
                                                   N.ptr(self.counts), _stream_ptr(self.stream)))
 
-    def pair_counts(self, S):
+    def pair_counts(self, S, overwrite=False):
+        """Pair counts of the batch into self.pairs: added (default) or, with ``overwrite``, stored
+        (upper triangle incl. the diagonal; CSA_PAIR_OVERWRITE, no zero-fill needed)."""
         nblk = (int(S) + 63) // 64
         L = N.lib()
         need = int(L.csa_pair_scratch_bytes(self.enc.n, nblk, self.pair_engine))
         assert need <= self.pair_scratch.numel() * 4
-        N.check(L.csa_pair_counts_ex_async(N.ptr(self.xt), nblk, self.enc.n, N.ptr(self.pairs), self.pair_engine,
+        N.check(L.csa_pair_counts_ex_async(N.ptr(self.xt), nblk, self.enc.n, N.ptr(self.pairs),
+                                           self.pair_engine | (N.CSA_PAIR_OVERWRITE if overwrite else 0),
                                            N.ptr(self.pair_scratch), self.pair_scratch.numel() * 4,
                                            _stream_ptr(self.stream)))
 

@@ -165,9 +165,14 @@ int csa_transpose_count_async(const uint64_t *d_panels, uint64_t n_panels, int32
  * csa_pair_scratch_bytes bytes of device memory) each split writes an int32
  * partial block and a reduce kernel sums them; with d_scratch == NULL the
  * splits add into d_pairs with int64 atomics.  csa_pair_counts_async =
- * engine FP4, no scratch. */
+ * engine FP4, no scratch.  engine | CSA_PAIR_OVERWRITE stores instead of
+ * accumulating: on return d_pairs holds exactly this batch's counts for i <= j
+ * (the reduce kernel writes every element of the upper-triangular blocks; without
+ * scratch the call zero-fills d_pairs first), so a caller that counts each batch
+ * afresh needs no n*n zero-fill of its own. */
 #define CSA_PAIR_FP4 0u
 #define CSA_PAIR_I8 1u
+#define CSA_PAIR_OVERWRITE 0x100u
 uint64_t csa_pair_scratch_bytes(int32_t n, uint64_t n_blocks, uint32_t engine);
 int csa_pair_counts_ex_async(const uint64_t *d_xt, uint64_t n_blocks, int32_t n, int64_t *d_pairs,
                              uint32_t engine, void *d_scratch, uint64_t scratch_bytes, void *stream);

@@ -24,13 +24,13 @@ def _cpu_pairs(xt, n, npad, rows=None):
     return np.rint(X.T @ X).astype(np.int64)                      # BLAS; exact below 2^53
 
 
-def _run(xt_np, n, engine, scratch):
+def _run(xt_np, n, engine, scratch, init=0):
     import torch
     N = pkg("_native")
     L = N.lib()
     nblk = xt_np.shape[0]
     xt = torch.from_numpy(xt_np.view(np.int64).copy()).cuda()
-    pairs = torch.zeros(n * n, dtype=torch.int64, device="cuda")
+    pairs = torch.full((n * n,), init, dtype=torch.int64, device="cuda")
     sb = int(L.csa_pair_scratch_bytes(n, nblk, engine))
     scr = torch.empty((sb + 3) // 4, dtype=torch.int32, device="cuda") if scratch else None
     N.check(L.csa_pair_counts_ex_async(N.ptr(xt), nblk, n, N.ptr(pairs), engine, N.ptr(scr),
@@ -55,6 +55,27 @@ def test_pair_engines_exact(gpu_available, n, S, engine, scratch):
     ref = _cpu_pairs(xt, n, npad)
     iu = np.triu_indices(n)
     assert np.array_equal(got[iu], ref[iu])
+
+
+@pytest.mark.parametrize("n,S", [(20, 1000), (1727, 20000)])
+@pytest.mark.parametrize("engine,scratch", [(0, True), (0, False), (1, True)])
+def test_pair_overwrite_ignores_prior_contents(gpu_available, n, S, engine, scratch):
+    """CSA_PAIR_OVERWRITE: the output holds exactly this batch's counts whatever it held before
+    (bench.py skips the n*n zero-fill this way); the plain mode adds onto the prior contents."""
+    N = pkg("_native")
+    npad = int(N.lib().csa_xt_pad(n))
+    nblk = (S + 63) // 64
+    rng = np.random.default_rng(n + S)
+    xt = rng.integers(0, 2 ** 64, size=(nblk, npad), dtype=np.uint64) & rng.integers(0, 2 ** 64, size=(nblk, npad),
+                                                                                     dtype=np.uint64)
+    if S % 64:
+        xt[-1, :] &= np.uint64((1 << (S % 64)) - 1)
+    ref = _cpu_pairs(xt, n, npad)
+    iu = np.triu_indices(n)
+    got = _run(xt, n, engine | N.CSA_PAIR_OVERWRITE, scratch, init=-12345)
+    assert np.array_equal(got[iu], ref[iu])
+    got_add = _run(xt, n, engine, scratch, init=7)
+    assert np.array_equal(got_add[iu], ref[iu] + 7)
 
 
 def test_pair_fp4_exact_beyond_f32_range(gpu_available):
