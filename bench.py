@@ -60,8 +60,10 @@ def parse():
     ap.add_argument("--no-overlap", action="store_true",
                     help="run each step's draw after the previous step's counting (default: the draw of step "
                          "i+1 runs on a second stream, into a second panel buffer, while step i is counted)")
-    ap.add_argument("--bufs", type=int, default=int(os.environ.get("CSA_BENCH_BUFS", "2")),
+    ap.add_argument("--bufs", type=int, default=int(os.environ.get("CSA_BENCH_BUFS", "3")),
                     help="panel buffers in the --overlap pipeline (draw i+1 waits for the counting of step i+1-bufs)")
+    ap.add_argument("--count-priority", type=int, default=int(os.environ.get("CSA_BENCH_PRIO", "0")),
+                    help="1: the counting stream of the --overlap pipeline is a high-priority stream")
     ap.add_argument("--iso-steps", type=int, default=2,
                     help="serial steps after the timed region that measure each kernel alone (not in `value`)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -152,6 +154,10 @@ def main():
     enc.check_quotas(k)
     want_pairs = not args.no_pairs
     stream = torch.cuda.current_stream(dev)
+    if not args.no_overlap and args.count_priority:
+        # the counting stream gets the high-priority queue: its workgroups are dispatched ahead of the
+        # draw's as draw workgroups retire (the draw holds every VGPR while it runs)
+        stream = torch.cuda.Stream(dev, priority=-1)
     engine_id, engine_peak, engine_desc = PAIR_ENGINES[args.pair_engine]
     pipe = Dv.DevicePipeline(enc, k, S, want_pairs=want_pairs, want_unique=True, device=dev, stream=stream,
                              pair_engine=engine_id)
@@ -209,8 +215,9 @@ def main():
         if evs:
             evs[5].record(stream)
         if world > 1:
-            last["unique"] = Dd.combine(pipe.counts, pipe.pairs, pipe.hashes[: 2 * S], table=table, stream=stream,
-                                        pair_bound=S * world)[2]
+            with torch.cuda.stream(stream):   # collectives order on the current stream
+                last["unique"] = Dd.combine(pipe.counts, pipe.pairs, pipe.hashes[: 2 * S], table=table,
+                                            stream=stream, pair_bound=S * world)[2]
         if evs:
             evs[6].record(stream)
             log.append(evs)

@@ -1509,7 +1509,13 @@ int launch_draw(const csa_instance *I, int32_t k, uint64_t seed, uint64_t panel_
     HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, cfg.fn, threads, lds));
     HIPCHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, I->device));
     const uint64_t want = (n_panels + groups_wg - 1) / groups_wg;
-    const uint64_t cap = (uint64_t)std::max(per_cu, 1) * (uint64_t)std::max(cus, 1);
+    uint64_t cap = (uint64_t)std::max(per_cu, 1) * (uint64_t)std::max(cus, 1);
+    // CSA_DRAW_WAVES=m: m resident grids' worth of workgroups; 0 = one workgroup per 128 panels (not
+    // persistent).  Default: 0 for the lane kernel -- sf_e 10^6 panels: 4.47 ms vs 5.05 ms persistent,
+    // and retiring workgroups let a concurrent stream's kernels in -- 1 (persistent) for the others
+    long waves = cfg.lane ? 0 : 1;
+    if (const char *e = getenv("CSA_DRAW_WAVES")) waves = atol(e);
+    cap = waves <= 0 ? want : cap * (uint64_t)waves;
     const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min(want, cap));
     void *args[] = {&A};
     HIPCHK(hipLaunchKernel(cfg.fn, dim3(grid), dim3(threads), args, lds, stream));
