@@ -2,28 +2,31 @@
 
 One "step" = one pass of the hot path (analysis.py:162-191) over one batch of
 synthetic-instance panels per GPU, entirely on the device:
-draw (with restarts) -> panel hashes -> per-person counts -> pair counts X^T X
-(fp4 MFMA) -> distinct-panel count, plus (N > 1) the RCCL exchange (all_reduce of
-counts and packed pairs, all_to_all of panel hashes to their owner rank + device
-dedupe + all_reduce).  By default step i+1's draw runs on a second stream while
-step i is counted (as csa_legacy_sample pipelines its chunks); --no-overlap
-serialises them.
+draw (with restarts; pick lists) -> pack (packed panels + 128-bit hashes) ->
+bit transpose + per-person counts -> pair counts X^T X (fp4 MFMA) -> exact
+distinct-panel count, plus (N > 1) the exchange (RCCL all_reduce of counts and
+packed pairs, all_to_all of every panel to its owner rank + exact owner dedupe +
+all_reduce).  The draws run on their own stream, enqueued --bufs - 1 steps ahead
+of the counting, so the draw stream never waits for the host (the exchange's
+size negotiation synchronises the host with the counting stream only);
+--no-overlap serialises everything on one stream.
 
     python bench.py [--gpus N --steps K --warmup W] [--config sf_e_110] [--panels P]
 
 Default workload: BASELINE config 2 -- the sf_e_110-shape instance
 (tests/golden/instances/sf_e_110, n=1727 k=110 C=7 F=31; synthetic, the real
-pool is withheld) at 10^6 panels per GPU per step (weak scaling).  Rank 0
-prints ONE JSON line.  The instance and every buffer are resident in HBM
-before the timed region.
+pool is withheld) at 10^6 panels per GPU per step (weak scaling), 400 timed
+steps (~2 s).  Rank 0 prints ONE JSON line.  The instance and every buffer are
+resident in HBM before the timed region.
 """
 import argparse
-import ctypes
 import glob
+import hashlib
 import importlib
 import json
 import os
 import platform
+import subprocess
 import sys
 import time
 
@@ -50,24 +53,22 @@ CONFIGS = {
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=400)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="sf_e_110", choices=sorted(CONFIGS))
     ap.add_argument("--panels", type=int, default=0, help="panels per GPU per step (0 = config default)")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--no-pairs", action="store_true")
     ap.add_argument("--pair-engine", default="fp4", choices=sorted(PAIR_ENGINES))
     ap.add_argument("--no-overlap", action="store_true",
-                    help="run each step's draw after the previous step's counting (default: the draw of step "
-                         "i+1 runs on a second stream, into a second panel buffer, while step i is counted)")
-    ap.add_argument("--bufs", type=int, default=int(os.environ.get("CSA_BENCH_BUFS", "3")),
-                    help="panel buffers in the --overlap pipeline (draw i+1 waits for the counting of step i+1-bufs)")
-    ap.add_argument("--count-priority", type=int, default=int(os.environ.get("CSA_BENCH_PRIO", "0")),
-                    help="1: the counting stream of the --overlap pipeline is a high-priority stream")
+                    help="serialise every stage on one stream (default: draws on their own stream, "
+                         "--bufs - 1 steps ahead of the counting)")
+    ap.add_argument("--bufs", type=int, default=3, help="panel buffers of the draw/count pipeline")
     ap.add_argument("--iso-steps", type=int, default=2,
                     help="serial steps after the timed region that measure each kernel alone (not in `value`)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample duration")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target duration of each CPU-baseline leg")
+    ap.add_argument("--no-api", action="store_true", help="skip the legacy_probabilities end-to-end leg")
     return ap.parse_args()
 
 
@@ -82,42 +83,130 @@ def cpu_model():
     return platform.processor() or "unknown"
 
 
+def cpu_quota():
+    """CPUs the cgroup lets this process use (cpu.max), or None when unlimited / unknown."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as fh:
+            q, p = fh.read().split()[:2]
+        return None if q == "max" else round(int(q) / int(p), 2)
+    except (OSError, ValueError):
+        return None
+
+
+def source_sha():
+    """Digest of the kernel sources: a committed PMC profile is only used for the same kernels."""
+    h = hashlib.sha256()
+    for path in sorted(glob.glob(os.path.join(REPO, PKG, "csrc", "*"))):
+        with open(path, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
+_PY_LEG = r"""
+import json, sys, time
+sys.path.insert(0, %(repo)r)
+from oracle.legacy_oracle import read_instance, legacy_probabilities
+o = read_instance(%(cat)r, %(resp)r, %(k)d)
+t = time.perf_counter()
+r = legacy_probabilities(o, %(S)d, %(seed)d, panel_begin=%(begin)d)
+print(json.dumps({"seconds": time.perf_counter() - t, "unique": r.unique}))
+"""
+
+
+def python_leg(d, k, seed, S, procs):
+    """The Python restatement of the reference loop (oracle/legacy_oracle.py: draws, Counter, pair
+    counts, distinct set) in `procs` single-threaded processes of S panels each, started together."""
+    env = dict(os.environ, OMP_NUM_THREADS="1", OPENBLAS_NUM_THREADS="1", MKL_NUM_THREADS="1")
+    cat, resp = os.path.join(d, "categories.csv"), os.path.join(d, "respondents.csv")
+    t = time.perf_counter()
+    ps = [subprocess.Popen([sys.executable, "-c", _PY_LEG % dict(repo=REPO, cat=cat, resp=resp, k=k, S=S, seed=seed,
+                                                                 begin=j * S)],
+                           env=env, stdout=subprocess.PIPE, stderr=subprocess.DEVNULL) for j in range(procs)]
+    outs = [p.communicate()[0] for p in ps]
+    wall = time.perf_counter() - t
+    if any(p.returncode for p in ps):
+        raise RuntimeError("python CPU-baseline leg failed")
+    inner = max(json.loads(o)["seconds"] for o in outs)
+    return procs * S / wall, wall, inner
+
+
 def cpu_baseline(inst_dir, k, seed, target_s, want_pairs):
-    """C oracle (the 'port') on the host cores: draw + counts + pairs + unique on a bounded sample."""
+    """CPU legs on this host, bounded samples of the same workload:
+    the C OpenMP port on every host core (`value`, `cores`), the Python restatement of the
+    reference loop on one core, and one Python process per host core."""
     from oracle import coracle
     from oracle.legacy_oracle import read_instance
     d = os.path.join(REPO, "tests", "golden", "instances", inst_dir)
     o = read_instance(os.path.join(d, "categories.csv"), os.path.join(d, "respondents.csv"), k)
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
-    threads = max(1, min(threads, 16))
+    cores = len(os.sched_getaffinity(0))
 
     def run(S):
         t = time.perf_counter()
-        rc, panels, _, _ = coracle.draw(o, k, seed, 0, S, threads=threads)
+        rc, panels, _, _ = coracle.draw(o, k, seed, 0, S, threads=cores)
         assert rc == 0
         coracle.counts(panels, o.n)
         if want_pairs:
-            coracle.pairs(panels, o.n, threads=threads)
+            coracle.pairs(panels, o.n, threads=cores)
         coracle.unique(panels, o.n)
         return time.perf_counter() - t
 
-    probe = 2000
+    probe = 4000
     dt = run(probe)
-    S = int(min(max(probe, probe * target_s / max(dt, 1e-6)), 5 * 10 ** 6))
+    S = int(min(max(probe, probe * target_s / max(dt, 1e-6)), 10 ** 7))
     dt = run(S)
-    return {"value": S / dt, "unit": "panels/s", "cores": threads, "kind": "port",
-            "sample": "%d panels of %s (draw+counts+%sunique), C oracle OpenMP x%d on %s" % (
-                S, inst_dir, "pairs+" if want_pairs else "", threads, cpu_model()),
-            "seconds": round(dt, 3)}
+    out = {"value": S / dt, "unit": "panels/s", "cores": cores, "kind": "port",
+           "sample": "%d panels of %s (draw+counts+%sunique), C oracle OpenMP x%d threads on %s" % (
+               S, inst_dir, "pairs+" if want_pairs else "", cores, cpu_model()),
+           "seconds": round(dt, 3), "cpu_model": cpu_model(), "host_cpus_affinity": cores,
+           "cgroup_cpu_quota": cpu_quota()}
+    # Python restatement: probe, then ~target_s per process
+    rate1, w1, _ = python_leg(d, k, seed, 20, 1)
+    S1 = max(20, int(rate1 * target_s * 0.8))
+    rate1, w1, _ = python_leg(d, k, seed, S1, 1)
+    out["python_1core"] = {"value": rate1, "unit": "panels/s", "cores": 1, "panels": S1, "seconds": round(w1, 3),
+                           "sample": "oracle/legacy_oracle.py (Python restatement of analysis.py:162-191), 1 process"}
+    Sp = max(10, int(rate1 * target_s * 0.5))
+    ratep, wp, innerp = python_leg(d, k, seed, Sp, cores)
+    out["python_per_core"] = {"value": ratep, "unit": "panels/s", "cores": cores, "panels_per_process": Sp,
+                              "seconds": round(wp, 3), "slowest_process_seconds": round(innerp, 3),
+                              "sample": "%d single-threaded Python processes (one per host core) of %d panels" % (
+                                  cores, Sp)}
+    out["reference_python_note"] = ("the unmodified reference (Python, dict + deepcopy) ran at 30.2 panels/s on one "
+                                    "core at this shape (SURVEY.md section 6, dev container)")
+    return out
 
 
-def load_pmc_traffic(config):
-    """HBM bytes per draw launch from a committed rocprofv3 --pmc summary (tools/pmc_summary.py)."""
+def load_pmc(config):
+    """Committed rocprofv3 --pmc summary (tools/make_pmc_profile.py) for this config."""
     path = os.path.join(REPO, "profiles", "pmc_%s.json" % config)
     if not os.path.exists(path):
         return None
     with open(path) as fh:
         return json.load(fh)
+
+
+def api_leg(P, A, inst, S, seed):
+    """legacy_probabilities(instance, S, seed) end to end (analysis.py:162 signature): first call,
+    then the steady state (cached encoding + device pipeline), then the host materialisation of the
+    n*n pair histogram and of the per-person dict."""
+    import torch
+    t = time.perf_counter()
+    A.legacy_probabilities(inst, S, seed)
+    first = time.perf_counter() - t
+    runs = []
+    for _ in range(3):
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        alloc, found, hist = A.legacy_probabilities(inst, S, seed)
+        runs.append(time.perf_counter() - t)
+    t = time.perf_counter()
+    hist.upper()
+    mat = time.perf_counter() - t
+    return {"call": "legacy_probabilities(sf_e_110 instance, %d, %d)" % (S, seed), "first_call_ms": first * 1e3,
+            "ms": min(runs) * 1e3, "ms_runs": [r * 1e3 for r in runs], "pair_histogram_materialise_ms": mat * 1e3,
+            "unique": len(found), "note": "returns the alloc dict, the exact distinct count (found_panels decodes "
+                                          "the device panels when iterated) and a PairHistogram whose n*n matrix is "
+                                          "copied and divided on first access (pair_histogram_materialise_ms)"}
 
 
 def main():
@@ -144,6 +233,7 @@ def main():
             dist.init_process_group(backend)
 
     P = importlib.import_module(PKG)
+    A = importlib.import_module(PKG + ".analysis")
     Dv = importlib.import_module(PKG + ".device")
     Dd = importlib.import_module(PKG + ".distributed")
     inst_dir, k, default_panels = CONFIGS[args.config]
@@ -154,85 +244,103 @@ def main():
     enc.check_quotas(k)
     want_pairs = not args.no_pairs
     stream = torch.cuda.current_stream(dev)
-    if not args.no_overlap and args.count_priority:
-        # the counting stream gets the high-priority queue: its workgroups are dispatched ahead of the
-        # draw's as draw workgroups retire (the draw holds every VGPR while it runs)
-        stream = torch.cuda.Stream(dev, priority=-1)
     engine_id, engine_peak, engine_desc = PAIR_ENGINES[args.pair_engine]
     pipe = Dv.DevicePipeline(enc, k, S, want_pairs=want_pairs, want_unique=True, device=dev, stream=stream,
                              pair_engine=engine_id)
     table = Dd.HashTable(S * world, dev) if world > 1 else None
-
     draw_name = pipe.draw_kernel_name()   # the kernel csa_draw_async launches (matches rocprofv3 names)
-    stages = ["draw", "hash", "xt_count", "pairs", "unique", "exchange"]
-    ev_log = []
-    last = {"unique": pipe.unique}
+    split = pipe.split_draw
+    W = enc.W
 
-    # --overlap (default): step i+1's draw (draw_stream, panel buffer (i+1) % 2) runs while step i is
-    # hashed / counted / paired / exchanged on `stream`; every step still does all of its work and
-    # the timed region still ends with a device-wide synchronize
     overlap = not args.no_overlap
+    nb = max(args.bufs, 2) if overlap else 1
+    ahead = nb - 1                                  # draws enqueued ahead of the counting
     draw_stream = torch.cuda.Stream(dev) if overlap else stream
-    bufs = [pipe.panels] + [torch.empty_like(pipe.panels) for _ in range(max(args.bufs, 2) - 1)] if overlap \
-        else [pipe.panels]
-    drawn = [torch.cuda.Event() for _ in bufs]       # draw of the buffer finished (draw_stream)
-    counted = [torch.cuda.Event() for _ in bufs]     # counting of the buffer finished (stream)
+    pbufs = [pipe.panels] + [torch.empty_like(pipe.panels) for _ in range(nb - 1)]
+    hbufs = [pipe.hashes] + [torch.empty_like(pipe.hashes) for _ in range(nb - 1)]
+    drawn = [torch.cuda.Event() for _ in range(nb)]    # draw + pack of the buffer finished (draw stream)
+    counted = [torch.cuda.Event() for _ in range(nb)]  # counting of the buffer finished (counting stream)
+    stages = ["draw", "pack", "xt_count", "pairs", "unique", "exchange"]
     with torch.cuda.stream(stream):
         pipe.status.zero_()
+    last = {"unique": pipe.unique}
 
-    def step(i, log, ov=overlap):
-        begin = (i * world + rank) * S            # global panel indices, distinct per step and rank
-        evs = [torch.cuda.Event(enable_timing=True) for _ in range(len(stages) + 2)] if log is not None else None
-        b = i % len(bufs) if ov else 0
-        ds = draw_stream if ov else stream
-        pipe.panels = bufs[b]
-        if ov:
-            ds.wait_event(counted[b])             # step i-2 is done reading this buffer
-        if evs:
-            evs[-1].record(ds)
-        pipe.draw(args.seed, begin, S, stream=ds)
-        if evs:
-            evs[1].record(ds)
+    def Ev():
+        return torch.cuda.Event(enable_timing=True)
+
+    def enqueue_draw(j, rec):
+        b = j % nb
+        ds = draw_stream
+        ds.wait_event(counted[b])                 # step j - nb is done reading this buffer
+        pipe.panels, pipe.hashes = pbufs[b], hbufs[b]
+        begin = (j * world + rank) * S            # global panel indices, distinct per step and rank
+        e = [Ev(), Ev(), Ev()] if rec is not None else None
+        if e:
+            e[0].record(ds)
+        if split:
+            pipe.draw_picks(args.seed, begin, S, stream=ds)
+            if e:
+                e[1].record(ds)
+            pipe.pack(S, stream=ds)
+        else:
+            pipe.draw(args.seed, begin, S, stream=ds)
+            if e:
+                e[1].record(ds)
+        if e:
+            e[2].record(ds)
+            rec[j] = {"draw": (e[0], e[1]), "pack": (e[1], e[2])}
         drawn[b].record(ds)
+
+    def enqueue_count(j, rec):
+        b = j % nb
         stream.wait_event(drawn[b])
-        # the pair matrix is not zero-filled: pair_counts stores this step's counts (overwrite), which
-        # keeps a 24 MB fill (2.6 ms when it shares the CUs with the next draw) off the counting stream
+        pipe.panels, pipe.hashes = pbufs[b], hbufs[b]
+        e = [Ev() for _ in range(5)] if rec is not None else None
         pipe.reset(status=False, pairs=False)
-        if evs:
-            evs[0].record(stream)
-        pipe.hash(S)
-        if evs:
-            evs[2].record(stream)
+        if e:
+            e[0].record(stream)
         pipe.transpose_count(S)
-        if evs:
-            evs[3].record(stream)
+        if e:
+            e[1].record(stream)
         if want_pairs:
+            # the pair matrix is stored (overwrite), not zero-filled and added
             pipe.pair_counts(S, overwrite=True)
-        if evs:
-            evs[4].record(stream)
+        if e:
+            e[2].record(stream)
         if world == 1:
             pipe.unique_count(S)
-        if evs:
-            evs[5].record(stream)
+        if e:
+            e[3].record(stream)
         if world > 1:
             with torch.cuda.stream(stream):   # collectives order on the current stream
-                last["unique"] = Dd.combine(pipe.counts, pipe.pairs, pipe.hashes[: 2 * S], table=table,
-                                            stream=stream, pair_bound=S * world)[2]
-        if evs:
-            evs[6].record(stream)
-            log.append(evs)
+                last["unique"] = Dd.combine(pipe.counts, pipe.pairs, pipe.hashes[: 2 * S], pipe.panels[: S * W], W,
+                                            table=table, stream=stream, pair_bound=S * world, status=pipe.status)[2]
+        if e:
+            e[4].record(stream)
+            rec[j].update({"xt_count": (e[0], e[1]), "pairs": (e[1], e[2]), "unique": (e[2], e[3]),
+                           "exchange": (e[3], e[4])})
         counted[b].record(stream)
 
-    for i in range(args.warmup):
-        step(i, None)
+    def run_steps(first, count, rec=None):
+        """Steps first .. first+count-1: draws `ahead` steps before their counting."""
+        for j in range(first, min(first + ahead, first + count)):
+            enqueue_draw(j, rec)
+        for j in range(first, first + count):
+            if j + ahead < first + count and ahead:
+                enqueue_draw(j + ahead, rec)
+            if not ahead:
+                enqueue_draw(j, rec)
+            enqueue_count(j, rec)
+
+    run_steps(0, args.warmup)
     torch.cuda.synchronize()
     pipe.check_status()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    log = {}
     t0 = time.perf_counter()
-    for i in range(args.steps):
-        step(args.warmup + i, ev_log)
+    run_steps(args.warmup, args.steps, log)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -249,35 +357,35 @@ def main():
     checks = {"last_step_unique": int(last["unique"].item()), "last_step_count_sum": int(pipe.counts.sum().item()),
               "last_step_pair_sum": int(torch.triu(pipe.pairs.view(enc.n, enc.n)).sum().item()) if want_pairs else None}
 
-    def stage_times(log):
-        """per-stage device time (ms) averaged over the logged steps (HIP events on the launch streams)"""
+    def stage_times(rec):
         out = {s: 0.0 for s in stages}
-        for evs in log:
-            for j, s in enumerate(stages):
-                a = evs[-1] if s == "draw" else evs[j] if s != "hash" else evs[0]
-                out[s] += a.elapsed_time(evs[j + 1]) / len(log)
+        for evs in rec.values():
+            for s in stages:
+                if s in evs:
+                    out[s] += evs[s][0].elapsed_time(evs[s][1]) / len(rec)
         return out
 
-    # stage times inside the timed region; with the two-stream pipeline the counting kernels share
-    # the CUs with the next step's draw, so their durations there are inflated.  A short serial pass
-    # AFTER the timed region (not part of `value`) measures every kernel alone on the device.
-    stage_pipe = stage_times(ev_log)
-    iso_log = []
-    if overlap:
-        torch.cuda.synchronize()
-        for i in range(args.iso_steps):
-            step(args.warmup + args.steps + i, iso_log, ov=False)
+    # stage times inside the timed region (HIP events on the streams the kernels run on); the
+    # counting kernels share the CUs with the next steps' draws there.  A short serial pass AFTER
+    # the timed region (not part of `value`) measures every kernel alone on the device.
+    stage_pipe = stage_times(log)
+    iso = {}
+    if overlap and args.iso_steps:
+        ahead_saved = ahead
+        ahead = 0
+        run_steps(args.warmup + args.steps, args.iso_steps, iso)
+        ahead = ahead_saved
         torch.cuda.synchronize()
         pipe.check_status()
-    stage_ms = stage_times(iso_log) if iso_log else stage_pipe
-    n, W = enc.n, enc.W
+    stage_ms = stage_times(iso) if iso else stage_pipe
+    n = enc.n
     npad = pipe.npad
     nblk = (S + 63) // 64
-    draw_bytes = S * 8 * W                                # packed panel per panel (written once)
-    hash_bytes = S * (8 * W + 16)                         # read the panel, write its 128-bit hash
-    xt_bytes = S * 8 * W + nblk * npad * 8 + n * 8        # read panels, write transposed bits + counts
-    pair_ops = S * n * (n + 1)                            # triangle form of 2*S*n^2 (BASELINE.md section 3)
-    uniq_bytes = S * (16 + 8 * 2)                         # hashes + table slot traffic (approx.)
+    draw_bytes = S * 2 * k if split else S * (8 * W + 16)   # pick lists written (or bitmasks + hashes)
+    pack_bytes = S * (2 * k + 8 * W + 16)                  # read the pick lists, write panels + hashes
+    xt_bytes = S * 8 * W + nblk * npad * 8 + n * 8         # read panels, write transposed bits + counts
+    pair_ops = S * n * (n + 1)                             # triangle form of 2*S*n^2
+    uniq_bytes = S * (16 + 8 * 2)                          # hashes + index / histogram traffic (approx.)
 
     def gbs(b, ms):
         return b / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
@@ -285,13 +393,16 @@ def main():
     kernels = {
         "draw": {"kernel": draw_name, "ms": stage_ms["draw"],
                  "panels_per_s": S / (stage_ms["draw"] * 1e-3) if stage_ms["draw"] else 0,
-                 "bound": "issue (VALU/LDS latency)", "hbm_GBps": gbs(draw_bytes, stage_ms["draw"])},
-        "hash": {"kernel": "panel_hash_kernel", "ms": stage_ms["hash"], "hbm_GBps": gbs(hash_bytes, stage_ms["hash"]),
-                 "frac": gbs(hash_bytes, stage_ms["hash"]) * 1e9 / HBM_PEAK},
-        "xt_count": {"ms": stage_ms["xt_count"], "hbm_GBps": gbs(xt_bytes, stage_ms["xt_count"]),
+                 "bound": "issue (VALU/LDS latency)", "hbm_GBps": gbs(draw_bytes, stage_ms["draw"]),
+                 "algorithmic_bytes": draw_bytes},
+        "xt_count": {"kernel": "xt_count_kernel", "ms": stage_ms["xt_count"], "hbm_GBps": gbs(xt_bytes, stage_ms["xt_count"]),
                      "frac": gbs(xt_bytes, stage_ms["xt_count"]) * 1e9 / HBM_PEAK},
         "unique": {"ms": stage_ms["unique"], "hbm_GBps": gbs(uniq_bytes, stage_ms["unique"])},
     }
+    if split:
+        kernels["pack"] = {"kernel": "picks_pack_kernel", "ms": stage_ms["pack"],
+                           "hbm_GBps": gbs(pack_bytes, stage_ms["pack"]),
+                           "frac": gbs(pack_bytes, stage_ms["pack"]) * 1e9 / HBM_PEAK}
     if want_pairs:
         tops = pair_ops / (stage_ms["pairs"] * 1e-3) / 1e12 if stage_ms["pairs"] else 0.0
         kernels["pairs_mfma"] = {"ms": stage_ms["pairs"], "engine": args.pair_engine, "operands": engine_desc,
@@ -302,38 +413,44 @@ def main():
                                          "ms includes the partial-block reduce kernel"}
     if world > 1:
         kernels["exchange"] = {"ms": stage_ms["exchange"]}
-    for key, st in (("draw", "draw"), ("hash", "hash"), ("xt_count", "xt_count"), ("unique", "unique"),
+    for key, st in (("draw", "draw"), ("pack", "pack"), ("xt_count", "xt_count"), ("unique", "unique"),
                     ("pairs_mfma", "pairs"), ("exchange", "exchange")):
         if key in kernels:
             kernels[key]["ms_in_timed_region"] = stage_pipe[st]
     kernel_timing = ("'ms' = each kernel alone (serial pass of %d steps after the timed region); "
-                         "'ms_in_timed_region' = HIP events on the launch streams inside the timed region, "
-                         "where the counting kernels share the CUs with the next step's draw" % len(iso_log)
-                         ) if iso_log else "HIP events on the launch stream inside the timed region (serial steps)"
-    dominant = max(("draw", "hash", "xt_count", "pairs", "unique"), key=lambda s: stage_pipe[s])
-    pmc = load_pmc_traffic(args.config)
+                     "'ms_in_timed_region' = HIP events on the launch streams inside the timed region, "
+                     "where the counting kernels share the CUs with the next steps' draws" % len(iso)
+                     ) if iso else "HIP events on the launch stream inside the timed region (serial steps)"
+    dominant = max(("draw", "pack", "xt_count", "pairs", "unique"), key=lambda s: stage_pipe[s])
+    pmc = load_pmc(args.config)
+    sha = source_sha()
+    pmc_ok = bool(pmc and pmc.get("source_sha") == sha and pmc.get("panels") == S)
     # the roofline's kernel duration is the one inside the timed region (what rocprofv3 averages)
     if dominant == "pairs":
         ach = pair_ops / (stage_pipe["pairs"] * 1e-3) / 1e12
         roof = {"kernel": "pair_mfma_kernel", "bound": "mfma", "achieved": ach, "peak": engine_peak / 1e12,
                 "unit": "TFLOP/s", "frac": ach * 1e12 / engine_peak, "traffic": None}
     else:
-        name = {"draw": draw_name, "hash": "panel_hash_kernel", "xt_count": "xt_count_kernel",
-                "unique": "unique_kernel"}[dominant]
-        b = {"draw": draw_bytes, "hash": hash_bytes, "xt_count": xt_bytes, "unique": uniq_bytes}[dominant]
+        name = {"draw": draw_name, "pack": "picks_pack_kernel", "xt_count": "xt_count_kernel",
+                "unique": "uq_dedupe_kernel"}[dominant]
+        b = {"draw": draw_bytes, "pack": pack_bytes, "xt_count": xt_bytes, "unique": uniq_bytes}[dominant]
         ach = gbs(b, stage_pipe[dominant])
         traffic = None
         pk = (pmc or {}).get("per_kernel", {}).get(name)
-        if pk and pmc.get("panels") == S:
-            traffic = pk.get("hbm_bytes_per_launch")     # committed rocprofv3 --pmc FETCH/WRITE passes
+        if pk and pmc_ok:
+            traffic = pk.get("hbm_bytes_per_launch")     # rocprofv3 --pmc FETCH/WRITE passes of these kernels
         roof = {"kernel": name, "bound": "hbm", "achieved": ach, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
-                "frac": ach * 1e9 / HBM_PEAK, "traffic": traffic}
+                "frac": ach * 1e9 / HBM_PEAK, "traffic": traffic, "algorithmic_bytes": b}
         if dominant == "draw":
             roof["note"] = ("the draw kernel has no HBM or MFMA roof: it is VALU/LDS issue-bound; 'achieved' is "
-                            "its packed-panel writes; issue_frac is the VALU issue-slot fraction from rocprofv3 PMC")
-            if pmc and pmc.get("draw_issue") and pmc.get("draw_kernel") == draw_name:
+                            "its algorithmic writes (2k B of pick list per panel) over its in-region time; "
+                            "issue_frac / mean_waves_per_simd come from rocprofv3 PMC passes of these kernel sources")
+            if pmc_ok and pmc.get("draw_issue") and pmc.get("draw_kernel") == draw_name:
                 kernels["draw"]["pmc_issue"] = pmc["draw_issue"]
                 roof["issue_frac"] = pmc["draw_issue"].get("valu_issue_frac")
+                roof["mean_waves_per_simd"] = pmc["draw_issue"].get("mean_waves_per_simd")
+    roof["pmc_source_sha"] = sha
+    roof["pmc_matches_sources"] = pmc_ok
 
     total = S * world * args.steps
     result = {
@@ -352,8 +469,8 @@ def main():
         "config": {"workload": "%s: %d LEGACY panels/GPU/step, k=%d, n=%d, C=%d, F=%d, counts+%sunique" % (
             args.config, S, k, n, enc.C, enc.F, "pairs+" if want_pairs else ""),
             "panels_per_gpu_per_step": S, "instance": inst_dir, "parallelism": "panel shards x%d" % world,
-            "pipeline": ("2 streams: step i+1 drawn while step i is hashed/counted/paired%s" % (
-                "/exchanged" if world > 1 else "")) if overlap else "serial"},
+            "pipeline": ("draws on their own stream, %d steps ahead of the counting%s" % (
+                ahead, " and the exchange" if world > 1 else "")) if overlap else "serial"},
         "roofline": roof,
         "kernels": kernels,
         "kernel_timing": kernel_timing,
@@ -362,6 +479,8 @@ def main():
     if want_pairs:
         result["xtx_mfma_util"] = kernels["pairs_mfma"]["mfma_util"]
         result["xtx_int8_peak_equiv"] = kernels["pairs_mfma"]["int8_peak_equiv"]
+    if rank == 0 and world == 1 and not args.no_api and args.config == "sf_e_110":
+        result["api"] = api_leg(P, A, inst, 10 ** 6, args.seed)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cb = cpu_baseline(inst_dir, k, args.seed, args.cpu_seconds, want_pairs)
         result["cpu_baseline"] = cb

@@ -50,6 +50,9 @@ SIGNATURES = {
     "csa_legacy_attempt": (ctypes.c_int, [_P, _I32, _U64, _U64, _U32, _P, _P, _P, _P, _P]),
     "csa_first_panel_not_in": (ctypes.c_int, [_P, _I32, _U64, _U64, _U64, _U32, _P, _U64, _U64, _P, _P]),
     "csa_draw_async": (ctypes.c_int, [_P, _I32, _U64, _U64, _U64, _U32, _P, _P, _P, _P, _P, _P]),
+    "csa_draw_picks_supported": (ctypes.c_int, [_P, _I32]),
+    "csa_draw_picks_async": (ctypes.c_int, [_P, _I32, _U64, _U64, _U64, _U32, _P, _P, _P, _P]),
+    "csa_picks_pack_async": (ctypes.c_int, [_P, _U64, _I32, _I32, _P, _P, _P]),
     "csa_panel_hash_async": (ctypes.c_int, [_P, _U64, _I32, _P, _P]),
     "csa_draw_kernel_name": (ctypes.c_int, [_P, _I32, ctypes.c_char_p, _U64]),
     "csa_xt_pad": (_I32, [_I32]),
@@ -57,10 +60,9 @@ SIGNATURES = {
     "csa_pair_scratch_bytes": (_U64, [_I32, _U64, _U32]),
     "csa_pair_counts_ex_async": (ctypes.c_int, [_P, _U64, _I32, _P, _U32, _P, _U64, _P]),
     "csa_pair_counts_async": (ctypes.c_int, [_P, _U64, _I32, _P, _P]),
-    "csa_unique_async": (ctypes.c_int, [_P, _P, _U64, _I32, _P, _U64, _P, _P]),
-    "csa_unique_hashes_async": (ctypes.c_int, [_P, _U64, _U32, _U32, _P, _U64, _P, _P]),
+    "csa_unique_async": (ctypes.c_int, [_P, _P, _U64, _I32, _P, _U64, _P, _P, _P]),
     "csa_pair_histogram_async": (ctypes.c_int, [_P, _I32, _P, _U64, _P, _P]),
-    "csa_hash_buckets_async": (ctypes.c_int, [_P, _U64, _U32, _P, _P, _P, _P]),
+    "csa_hash_buckets_async": (ctypes.c_int, [_P, _P, _U64, _I32, _U32, _P, _P, _P, _P, _P]),
     "csa_pairs_pack_async": (ctypes.c_int, [_P, _I32, _P, _P]),
     "csa_pairs_unpack_async": (ctypes.c_int, [_P, _I32, _P, _P]),
     "csa_status_decode": (ctypes.c_int, [_P]),

@@ -27,25 +27,49 @@ ProbAllocation = Dict
 class PairHistogram:
     """analysis.py:68-98 with a dense backing store.
 
-    ``counts`` is an (n, n) array whose strict upper triangle holds the pair
-    values (row-major i < j is the reference's key order, analysis.py:70);
-    the lower triangle is ignored.  Integer counts stay exact until
+    The (n, n) matrix's strict upper triangle holds the pair values (row-major
+    i < j is the reference's key order, analysis.py:70); the lower triangle is
+    ignored.  Integer counts stay exact until
     ``turn_into_probabilities_by_dividing_all_elements_by_given_number``
-    divides them (float64 true division, as the reference's ``/``).
+    divides them (float64 true division, as the reference's ``/``).  A
+    histogram built by ``legacy_probabilities`` keeps the device's integer
+    pair counts and materialises the host matrix (one copy + the division) on
+    first access, so a caller that only reads per-person probabilities or
+    ``len(found_panels)`` never moves the n*n matrix.
     """
 
     def __init__(self, number_of_agents, uniform_distribution=False, counts=None):
         n = int(number_of_agents)
         self.n = n
+        self._src = None        # lazily materialised integer counts (numpy or device tensor)
+        self._divs = []         # divisions pending on _src, applied in order at materialisation
+        self._mat = None
         if counts is not None:
-            self._m = np.asarray(counts)
-            assert self._m.shape == (n, n)
+            if hasattr(counts, "device") and not isinstance(counts, np.ndarray):
+                self._src = counts
+            else:
+                self._mat = np.asarray(counts)
+                assert self._mat.shape == (n, n)
         else:
-            self._m = np.zeros((n, n), np.int64)
+            self._mat = np.zeros((n, n), np.int64)
         self._counts = self._S = None   # integer pair counts and S when built by finish()
         if uniform_distribution:
             npairs = n * (n - 1) // 2
-            self._m = np.full((n, n), 1 / npairs if npairs else 0.0, np.float64)
+            self._src = None
+            self._mat = np.full((n, n), 1 / npairs if npairs else 0.0, np.float64)
+
+    @property
+    def _m(self):
+        if self._mat is None:
+            m = self._src.cpu().numpy().reshape(self.n, self.n)
+            for d in self._divs:
+                m = m / d
+            self._mat, self._src, self._divs = m, None, []
+        return self._mat
+
+    @_m.setter
+    def _m(self, value):
+        self._mat, self._src, self._divs = value, None, []
 
     # dict-compatible accessors -----------------------------------------------------------
     def _key(self, key):
@@ -67,7 +91,10 @@ class PairHistogram:
         self._m[i, j] = value
 
     def turn_into_probabilities_by_dividing_all_elements_by_given_number(self, num):
-        self._m = self._m / num
+        if self._mat is None:
+            self._divs.append(num)
+        else:
+            self._m = self._m / num
         self._counts = self._S = None
 
     def add_portfolio_of_panels_to_histogram(self, portfolio, probabilities):
@@ -95,15 +122,17 @@ class PairHistogram:
         return {"n": self.n, "m": self._m}
 
     def __setstate__(self, st):
-        self.n, self._m = st["n"], st["m"]
+        self.n = st["n"]
+        self._src, self._divs, self._mat = None, [], st["m"]
         self._counts = self._S = None
 
 
 class PanelSet:
     """Set of distinct panels (found_panels, analysis.py:171,186), lazily materialised.
 
-    ``len()`` is the device's distinct-panel count; iteration / membership
-    decode the packed bitmasks (sorted agent-id tuples, as the reference).
+    ``len()`` is the device's exact distinct-panel count; iteration / membership
+    decode the packed bitmasks (host array, or a device tensor copied on first
+    use) into sorted agent-id tuples, as the reference's set holds them.
     """
 
     def __init__(self, unique_count, packed=None, n=0, agent_ids=None):
@@ -120,9 +149,14 @@ class PanelSet:
         if self._set is None:
             if self._packed is None:
                 raise RuntimeError("panels were not kept; only len() is available")
-            rows = np.unique(np.ascontiguousarray(self._packed), axis=0)
+            p = self._packed
+            if hasattr(p, "device") and not isinstance(p, np.ndarray):
+                W = (self._n + 63) // 64
+                p = p.cpu().numpy().view(np.uint64).reshape(-1, W)
+            rows = np.unique(np.ascontiguousarray(p), axis=0)
             ids = self._ids
-            self._set = {tuple(ids[p] for p in unpack_panel(r, self._n)) for r in rows}
+            self._set = {tuple(ids[q] for q in unpack_panel(r, self._n)) for r in rows}
+            self._packed = None
         return self._set
 
     def __iter__(self):
@@ -189,24 +223,73 @@ def legacy_sample_raw(enc, k, iterations, random_seed, panel_begin=0, want_pairs
     return LegacyRaw(counts, pairs, int(unique[0]), panels, attempts)
 
 
+def legacy_sample_device(enc, k, S, random_seed, keep_panels=True, chunk=1 << 20):
+    """One legacy_probabilities batch on the device through a DevicePipeline cached with the
+    encoding (picks / XT / scratch buffers reused across calls).  Panels and hashes of the whole
+    batch go to fresh device tensors (the exact distinct count needs all of them; with
+    ``keep_panels`` the returned PanelSet keeps the panel tensor and decodes it only when
+    iterated).  Returns LegacyRaw with host counts and device pair counts (PairHistogram
+    materialises them lazily)."""
+    import torch
+    from .device import DevicePipeline
+    from .distributed import HashTable
+    S = int(S)
+    pipe = getattr(enc, "_pipe", None)
+    C = max(1, min(S, int(chunk)))
+    if pipe is None or pipe.max_panels < C or pipe.k != int(k):
+        pipe = enc._pipe = DevicePipeline(enc, k, C, want_pairs=True, want_unique=True)
+    W = enc.W
+    dev = pipe.device
+    with torch.cuda.device(dev), torch.cuda.stream(pipe.stream):
+        panels = torch.empty(max(S * W, 1), dtype=torch.int64, device=dev)
+        hashes = torch.empty(max(2 * S, 2), dtype=torch.int64, device=dev)
+        pairs = torch.empty(enc.n * enc.n, dtype=torch.int64, device=dev)
+        pipe.reset(pairs=False)
+        own_p, own_h, own_pairs = pipe.panels, pipe.hashes, pipe.pairs
+        pipe.pairs = pairs
+        try:
+            for off in range(0, S, C):
+                ln = min(C, S - off)
+                pipe.panels, pipe.hashes = panels[off * W:(off + ln) * W], hashes[2 * off:2 * (off + ln)]
+                pipe.draw(random_seed, off, ln)
+                pipe.transpose_count(ln)
+                pipe.pair_counts(ln, overwrite=off == 0)
+            if S == 0:
+                pairs.zero_()
+            table = getattr(enc, "_table", None)
+            if table is None:
+                table = enc._table = HashTable(S, dev)
+            table.ensure(S)
+            table.count.zero_()
+            N.check(N.lib().csa_unique_async(N.ptr(hashes), N.ptr(panels), S, W, N.ptr(table.table), table.slots,
+                                             N.ptr(table.count), N.ptr(pipe.status),
+                                             ctypes.c_void_p(pipe.stream.cuda_stream)))
+            counts = pipe.counts.cpu().numpy()       # synchronises the stream
+            unique = int(table.count.item())
+            pipe.check_status()
+        finally:
+            pipe.panels, pipe.hashes, pipe.pairs = own_p, own_h, own_pairs
+    return LegacyRaw(counts, pairs.view(enc.n, enc.n), unique, panels[: S * W] if keep_panels else None, None)
+
+
 def legacy_probabilities(instance: Instance, iterations: int, random_seed: int,
                          keep_panels: bool = True) -> Tuple[ProbAllocation, PanelSet, PairHistogram]:
     """analysis.py:162-191 on the GPU.
 
     Returns ``({agent_id: count/S}, found_panels, pair_histogram)`` with the
-    pair histogram already divided by S, as the reference.  With
-    torch.distributed initialised and world size > 1 the panels are sharded
-    over ranks (see ``distributed.legacy_probabilities_distributed``).
+    pair histogram divided by S, as the reference.  With torch.distributed
+    initialised and world size > 1 the panels are sharded over ranks (see
+    ``distributed.legacy_probabilities_distributed``).
     """
     from . import distributed as D
     if D.world_size() > 1:
         return D.legacy_probabilities_distributed(instance, iterations, random_seed, keep_panels=keep_panels)
     seed(random_seed)
-    enc = encode(instance.categories, instance.agents)
+    enc = encode_cached(instance.categories, instance.agents)
     enc.check_quotas(instance.k)
     S = int(iterations)
     STREAM.take_panels(S)
-    raw = legacy_sample_raw(enc, instance.k, S, random_seed, want_pairs=True, want_panels=keep_panels)
+    raw = legacy_sample_device(enc, instance.k, S, random_seed, keep_panels=keep_panels)
     return finish(instance, enc, raw, S)
 
 

@@ -73,6 +73,7 @@ def load_legacy_npz(path, instance):
         S = int(z["S"])
         pairs = np.zeros((n, n), np.int64)
         pairs[np.triu_indices(n, 1)] = z["pair_upper"]
+        np.fill_diagonal(pairs, z["counts"])   # X^T X diagonal = per-person counts, as a fresh result
         panels = z["panels"] if "panels" in z.files else None
         raw = LegacyRaw(z["counts"].astype(np.int64), pairs, int(z["unique"]), panels, None)
     return finish(instance, enc, raw, S)
@@ -97,6 +98,7 @@ def run_legacy_or_retrieve(instance_name, instance, resample, directory="distrib
         S = int(iterations)
         STREAM.take_panels(S)
         raw = legacy_sample_raw(enc, instance.k, S, random_seed, want_pairs=True, want_panels=keep_panels)
+        np.fill_diagonal(raw.pairs, raw.counts)
         alloc, found_panels, pair_histogram = finish(instance, enc, raw, S)
         Path(directory).mkdir(parents=True, exist_ok=True)
         if fmt == "pickle":

@@ -128,6 +128,7 @@ struct DrawArgs {
     uint64_t *hashes;          // 2 x n_panels or null
     uint32_t *attempts;        // n_panels or null
     int32_t *picks;            // n_panels x k or null
+    uint16_t *picks16;         // draw_lane_kernel: n_panels x k pick lists (picks_pack_kernel -> panels)
     uint32_t *status;          // 4 words
     int32_t *sel_out, *rem_out;
     uint64_t *present_out;
@@ -137,7 +138,6 @@ struct DrawArgs {
 // A panel is drawn by a group of G lanes (G = 16: one DPP row; 32; 64 = whole wave).  All
 // cross-lane traffic inside a group is DPP (quad_perm / row mirrors / row_shr / row_bcast)
 // except the xor-16 / xor-32 butterfly levels of G = 32 / 64 (ds_bpermute).
-constexpr int kNone = 1 << 24;  // "no candidate" feature index
 
 template <int CTRL, int ROW_MASK = 0xF, bool BOUND_ZERO = false>
 __device__ __forceinline__ int dpp(int old, int v) {
@@ -534,7 +534,6 @@ __global__ __launch_bounds__(draw_threads(FPL, WPL), draw_occupancy(FPL, WPL)) v
     }
 }
 
-#include "draw_batch.inc"
 #include "draw_lane.inc"
 
 // 128-bit panel hashes (the draw_kernel's in-kernel hash, for the batch kernel's panels): a
@@ -645,7 +644,7 @@ typedef float v16f __attribute__((ext_vector_type(16)));
 
 constexpr int kPairBlock = 256;   // output block per workgroup
 constexpr int kPairThreads = 512;
-constexpr int kPairKB = 8;        // default 64-panel blocks staged per barrier (template KB; 8: 0.76 vs 0.79 ms at sf_e)
+constexpr int kPairKB = 8;        // 64-panel blocks staged per barrier (8: 0.76 ms at sf_e vs 0.79 for 4 or 16)
 
 // int8 fragment (k-half ks, lane half h) of one XT word: dword q holds bits 4h+q, 4h+q+8,
 // 4h+q+16, 4h+q+24 of the 32-bit half ks as 0/1 bytes.  Any fixed bit -> k placement works
@@ -695,21 +694,15 @@ __global__ __launch_bounds__(kPairThreads) void pair_mfma_kernel(const uint64_t 
                                                                  uint64_t nblk, int n, int npad,
                                                                  int nbt, int nsplit,
                                                                  int64_t *__restrict__ pairs,
-                                                                 int32_t *__restrict__ part, int xcd_map) {
+                                                                 int32_t *__restrict__ part) {
     __shared__ uint64_t words[2][KB][2 * kPairBlock];
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-    int tri, split;
-    if (xcd_map) {
-        // workgroups are dispatched round-robin over the 8 XCDs (blockIdx % 8): give every
-        // workgroup of one XCD the same panel-block split (nsplit % 8 == 0), so the 7-fold re-reads
-        // of each XT row block by the triangle blocks of that split hit the XCD's own L2
-        const int ntri = nbt * (nbt + 1) / 2, r = (int)(blockIdx.x >> 3);
-        tri = r % ntri;
-        split = (int)(blockIdx.x & 7) + 8 * (r / ntri);
-    } else {
-        tri = (int)blockIdx.x / nsplit;
-        split = (int)blockIdx.x - tri * nsplit;
-    }
+    // consecutive workgroups (dispatched round-robin over the 8 XCDs) take the splits of one
+    // block; an XCD-grouped mapping (every workgroup of an XCD on one split, so the XT re-reads of
+    // that split stay in its L2) measured 0.90 vs 0.82 ms at sf_e: it needs nsplit % 8 == 0 and
+    // left 32 CUs idle
+    const int tri = (int)blockIdx.x / nsplit;
+    const int split = (int)blockIdx.x - tri * nsplit;
     const int item = tri * nsplit + split;
     int bi, bj;
     tri_block(tri, nbt, bi, bj);
@@ -829,125 +822,7 @@ __global__ __launch_bounds__(kPairThreads) void pair_mfma_kernel(const uint64_t 
 }
 
 // Sum the nsplit int32 partial tiles of every upper-triangular block into the int64 output
-// (+=; each output element is owned by exactly one thread).  HBM-bound.
-// Wide variant of the fp4 engine: 4 waves per workgroup, each a 128 x 128 tile (4 x 4
-// accumulators = 256 accumulation registers, one wave per SIMD), so a word's 8 fragments feed 16
-// MFMAs (0.5 fragments per MFMA instead of 0.75): the fragment expansion is the VALU cost that
-// bounds pair_mfma_kernel.  Same staging, partial blocks and exactness bound.
-template <bool PARTIAL, int KB>
-__global__ __launch_bounds__(256, 1) void pair_mfma_wide_kernel(const uint64_t *__restrict__ xt, uint64_t nblk, int n,
-                                                                int npad, int nbt, int nsplit,
-                                                                int64_t *__restrict__ pairs,
-                                                                int32_t *__restrict__ part, int xcd_map) {
-    __shared__ uint64_t words[2][KB][2 * kPairBlock];
-    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-    int tri, split;
-    if (xcd_map) {
-        const int ntri = nbt * (nbt + 1) / 2, r = (int)(blockIdx.x >> 3);
-        tri = r % ntri;
-        split = (int)(blockIdx.x & 7) + 8 * (r / ntri);
-    } else {
-        tri = (int)blockIdx.x / nsplit;
-        split = (int)blockIdx.x - tri * nsplit;
-    }
-    const int item = tri * nsplit + split;
-    int bi, bj;
-    tri_block(tri, nbt, bi, bj);
-    const int I0 = bi * kPairBlock, J0 = bj * kPairBlock;
-    const uint64_t per = (nblk + nsplit - 1) / nsplit;
-    const uint64_t kb0 = min(nblk, (uint64_t)split * per), kb1 = min(nblk, kb0 + per);
-
-    v16f acc[4][4];
-#pragma unroll
-    for (int a = 0; a < 4; ++a)
-#pragma unroll
-        for (int b = 0; b < 4; ++b)
-#pragma unroll
-            for (int v = 0; v < 16; ++v) acc[a][b][v] = 0.0f;
-
-    const int wr = wave >> 1, wc = wave & 1;
-    const int r32 = lane & 31, h = lane >> 5;
-    uint64_t nwr[KB], nwc[KB];  // this thread stages row word I0 + t and column word J0 + t
-    const uint64_t nst = (kb1 - kb0 + KB - 1) / KB;
-    auto load_stage = [&](uint64_t s) {
-#pragma unroll
-        for (int j = 0; j < KB; ++j) {  // blocks past the split's end stage as zero words
-            const uint64_t b = kb0 + s * KB + j;
-            nwr[j] = b < kb1 ? xt[b * (uint64_t)npad + I0 + t] : 0ull;
-            nwc[j] = b < kb1 ? xt[b * (uint64_t)npad + J0 + t] : 0ull;
-        }
-    };
-    if (nst) {
-        load_stage(0);
-#pragma unroll
-        for (int j = 0; j < KB; ++j) {
-            words[0][j][t] = nwr[j];
-            words[0][j][kPairBlock + t] = nwc[j];
-        }
-        if (nst > 1) load_stage(1);
-    }
-    __syncthreads();
-    for (uint64_t s = 0; s < nst; ++s) {
-        const int buf = (int)(s & 1);
-#pragma unroll
-        for (int j = 0; j < KB; ++j) {
-            const uint32_t *w32 = reinterpret_cast<const uint32_t *>(words[buf][j]) + h;
-            v8i fa[4], fb[4];
-#pragma unroll
-            for (int x = 0; x < 4; ++x) fa[x] = f4_frag_a(w32[2 * (128 * wr + 32 * x + r32)]);
-#pragma unroll
-            for (int y = 0; y < 4; ++y) fb[y] = f4_frag_b(w32[2 * (kPairBlock + 128 * wc + 32 * y + r32)]);
-#pragma unroll
-            for (int a = 0; a < 4; ++a)
-#pragma unroll
-                for (int b = 0; b < 4; ++b)
-                    acc[a][b] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(fa[a], fb[b], acc[a][b], 4, 4, 0,
-                                                                                0x7F7F7F7F, 0, 0x7F7F7F7F);
-            if (j == 0) {  // hand the prefetched stage to LDS, prefetch the one after
-                if (s + 1 < nst) {
-#pragma unroll
-                    for (int jj = 0; jj < KB; ++jj) {
-                        words[buf ^ 1][jj][t] = nwr[jj];
-                        words[buf ^ 1][jj][kPairBlock + t] = nwc[jj];
-                    }
-                }
-                if (s + 2 < nst) load_stage(s + 2);
-            }
-        }
-        __syncthreads();
-    }
-    // C/D layout (gfx950): col = lane & 31, row = (v&3) + 8*(v>>2) + 4*(lane>>5)
-    const int rloc = 128 * wr + 4 * h, cloc = 128 * wc + r32;
-    if constexpr (PARTIAL) {
-        int32_t *dst = part + (size_t)item * kPairBlock * kPairBlock;
-#pragma unroll
-        for (int a = 0; a < 4; ++a)
-#pragma unroll
-            for (int b = 0; b < 4; ++b)
-#pragma unroll
-                for (int v = 0; v < 16; ++v) {
-                    const int row = rloc + 32 * a + (v & 3) + 8 * (v >> 2);
-                    dst[row * kPairBlock + cloc + 32 * b] = (int)acc[a][b][v];
-                }
-    } else {
-#pragma unroll
-        for (int a = 0; a < 4; ++a)
-#pragma unroll
-            for (int b = 0; b < 4; ++b) {
-                const int col = J0 + cloc + 32 * b;
-#pragma unroll
-                for (int v = 0; v < 16; ++v) {
-                    const int row = I0 + rloc + 32 * a + (v & 3) + 8 * (v >> 2);
-                    const int val = (int)acc[a][b][v];
-                    if (val != 0 && row < n && col < n)
-                        atomicAdd(reinterpret_cast<unsigned long long *>(pairs + (uint64_t)row * n + col),
-                                  (unsigned long long)(long long)val);
-                }
-                __builtin_amdgcn_sched_barrier(0);
-            }
-    }
-}
-
+// (+=, or = with overwrite; each output element is owned by exactly one thread).  HBM-bound.
 __global__ __launch_bounds__(256) void pair_reduce_kernel(const int32_t *__restrict__ part, int n, int nbt,
                                                           int nsplit, int64_t *__restrict__ pairs,
                                                           int overwrite) {
@@ -968,14 +843,14 @@ __global__ __launch_bounds__(256) void pair_reduce_kernel(const int32_t *__restr
 // ------------------------------------------------------------------------------------------
 // Distinct panels
 // ------------------------------------------------------------------------------------------
-// owner filter: only hashes with h1 % world == rank are inserted (multi-GPU partition)
+// one thread per panel: open addressing on `panel index + 1`, keyed by the 128-bit hash, exact
+// bitmask comparison on a hash match (small batches; the XMIN portfolio table)
 __global__ void unique_kernel(const uint64_t *__restrict__ hashes, const uint64_t *__restrict__ panels,
                               uint64_t S, int W, unsigned long long *__restrict__ table,
-                              uint64_t mask, unsigned long long *__restrict__ unique, uint32_t world,
-                              uint32_t rank) {
+                              uint64_t mask, unsigned long long *__restrict__ unique) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     bool inserted = false;
-    if (i < S && (world <= 1 || hashes[2 * i] % world == rank)) {
+    if (i < S) {
         const uint64_t h1 = hashes[2 * i], h2 = hashes[2 * i + 1];
         uint64_t slot = (h1 ^ (h2 >> 29)) & mask;
         for (uint64_t probe = 0; probe <= mask; ++probe) {
@@ -987,8 +862,7 @@ __global__ void unique_kernel(const uint64_t *__restrict__ hashes, const uint64_
             const uint64_t j = v - 1;
             if (hashes[2 * j] == h1 && hashes[2 * j + 1] == h2) {
                 bool same = true;
-                if (panels)
-                    for (int w = 0; w < W && same; ++w) same = panels[i * W + w] == panels[j * W + w];
+                for (int w = 0; w < W && same; ++w) same = panels[i * W + w] == panels[j * W + w];
                 if (same) break;
             }
             slot = (slot + 1) & mask;
@@ -1096,7 +970,8 @@ __global__ __launch_bounds__(kUqThreads) void uq_dedupe_kernel(const uint64_t *_
                                                                const uint64_t *__restrict__ panels, int W,
                                                                const uint32_t *__restrict__ idx,
                                                                const uint32_t *__restrict__ base,
-                                                               unsigned long long *__restrict__ unique) {
+                                                               unsigned long long *__restrict__ unique,
+                                                               uint32_t *__restrict__ status) {
     __shared__ uint32_t T[kUqTable];
     __shared__ uint32_t cnt;
     for (int t = threadIdx.x; t < kUqTable; t += blockDim.x) T[t] = 0;
@@ -1125,8 +1000,8 @@ __global__ __launch_bounds__(kUqThreads) void uq_dedupe_kernel(const uint64_t *_
             }
         }
         // a full table (more than kUqTable distinct panels in one partition; csa_unique_async
-        // sizes partitions at <= 2048 on average) poisons the count instead of dropping panels
-        if (!done) mine += 1u << 30;
+        // sizes partitions at <= 2048 on average) fails the call through the status block
+        if (!done) raise_status(status, CSA_E_UNSUPPORTED, 0xFFFFFFFFFFFFFFFFull);
     }
     atomicAdd(&cnt, mine);
     __syncthreads();
@@ -1192,15 +1067,19 @@ __global__ __launch_bounds__(256) void hash_owner_count_kernel(const uint64_t *_
         if (c[w]) atomicAdd(counts + w, (unsigned long long)c[w]);
 }
 
-__global__ __launch_bounds__(256) void hash_owner_scatter_kernel(const uint64_t *__restrict__ hashes, uint64_t n,
-                                                                 uint32_t world,
+__global__ __launch_bounds__(256) void hash_owner_scatter_kernel(const uint64_t *__restrict__ hashes,
+                                                                 const uint64_t *__restrict__ panels, uint64_t n,
+                                                                 int W, uint32_t world,
                                                                  unsigned long long *__restrict__ cursor,
-                                                                 uint64_t *__restrict__ out) {
+                                                                 uint64_t *__restrict__ out,
+                                                                 uint64_t *__restrict__ out_panels) {
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
         const uint64_t h1 = hashes[2 * i], h2 = hashes[2 * i + 1];
         const unsigned long long pos = atomicAdd(cursor + (h1 % world), 1ull);
         out[2 * pos] = h1;
         out[2 * pos + 1] = h2;
+        if (panels)  // the bitmask travels with its hash: the owner's dedupe compares bitmasks
+            for (int w = 0; w < W; ++w) out_panels[pos * W + w] = panels[i * W + w];
     }
 }
 
@@ -1270,6 +1149,7 @@ struct csa_instance {
     int32_t n = 0, C = 0, F = 0, W = 0, Ws = 0;
     int device = 0;
     std::vector<int32_t> pf, fmin, fmax, fcat, pool;
+    std::vector<int32_t> sel0;  // host copy of the initial "selected" counters (csa_instance_set_state)
     std::vector<uint64_t> featmask;  // F x Ws
     uint64_t *d_featmask = nullptr;
     int32_t *d_fmin = nullptr, *d_fmax = nullptr, *d_sel0 = nullptr, *d_rem0 = nullptr;
@@ -1280,9 +1160,16 @@ struct csa_instance {
     bool sel_over_max = false;  // some feature starts with selected > max (draw_lane_kernel excludes it)
     // grow-only device scratch + a stream for the repeated small host-API calls
     // (csa_first_panel_not_in: XMIN calls it 5n times)
-    void *scratch[8] = {};
-    size_t scratch_bytes[8] = {};
+    void *scratch[16] = {};   // slots 0-7: csa_first_panel_not_in; 8-15: csa_legacy_sample
+    size_t scratch_bytes[16] = {};
     hipStream_t stream = nullptr;
+    hipStream_t sdraw = nullptr, spost = nullptr;  // csa_legacy_sample's pipeline
+    hipEvent_t drawn = nullptr;
+    // draw_lane_kernel's pick lists (u16, n_panels x k), reused across draws (lane_picks)
+    uint16_t *d_picks16 = nullptr;
+    size_t picks_bytes = 0;
+    hipEvent_t picks_done = nullptr;
+    bool picks_pending = false;
 };
 
 namespace {
@@ -1315,42 +1202,38 @@ int check_k(const csa_instance *I, int32_t k) {
 
 struct DrawConfig {
     int G = 16, FPL = 1, WPL = 1;
-    bool batch = false;  // draw_batch_kernel (small groups) instead of draw_kernel
-    bool lane = false;   // draw_lane_kernel (G = 1): FPL / WPL hold its FN / WN
+    bool lane = false;  // draw_lane_kernel (2 lanes per panel): FPL / WPL hold its FN / WN
     const void *fn = nullptr;
 };
 
-template <int G, int FN>
-const void *lane_fn_w(int wn) {
-    if constexpr (FN / G < 4) {
-        return nullptr;
-    } else {
-        switch (wn) {
-            case 4: return reinterpret_cast<const void *>(&draw_lane_kernel<G, FN, 4>);
-            case 8: return reinterpret_cast<const void *>(&draw_lane_kernel<G, FN, 8>);
-            case 16: return reinterpret_cast<const void *>(&draw_lane_kernel<G, FN, 16>);
-            case 28: return reinterpret_cast<const void *>(&draw_lane_kernel<G, FN, 28>);
-            case 32: return reinterpret_cast<const void *>(&draw_lane_kernel<G, FN, 32>);
-            default: return nullptr;
-        }
-    }
+// holder-scan batch of the lane kernel: all of a lane's row words in one LDS round trip
+// (CSA_LANE_SKDIV > 1 splits them, trading a round trip for VGPRs)
+#ifndef CSA_LANE_SKDIV
+#define CSA_LANE_SKDIV 1
+#endif
+template <int FN, int WN>
+const void *lane_fn_wn() {
+    constexpr int SK = (WN / 2 + CSA_LANE_SKDIV - 1) / CSA_LANE_SKDIV;
+    return reinterpret_cast<const void *>(&draw_lane_kernel<FN, WN, SK>);
 }
 
-template <int G>
-const void *lane_fn_g(int fn_, int wn) {
-    switch (fn_) {
-        case 8: return lane_fn_w<G, 8>(wn);
-        case 16: return lane_fn_w<G, 16>(wn);
-        case 32: return lane_fn_w<G, 32>(wn);
+template <int FN>
+const void *lane_fn_w(int wn) {
+    switch (wn) {
+        case 4: return lane_fn_wn<FN, 4>();
+        case 8: return lane_fn_wn<FN, 8>();
+        case 16: return lane_fn_wn<FN, 16>();
+        case 28: return lane_fn_wn<FN, 28>();
+        case 32: return lane_fn_wn<FN, 32>();
         default: return nullptr;
     }
 }
 
-const void *lane_fn(int g, int fn_, int wn) {
-    switch (g) {
-        case 1: return lane_fn_g<1>(fn_, wn);
-        case 2: return lane_fn_g<2>(fn_, wn);
-        case 4: return lane_fn_g<4>(fn_, wn);
+const void *lane_fn(int fn_, int wn) {
+    switch (fn_) {
+        case 8: return lane_fn_w<8>(wn);
+        case 16: return lane_fn_w<16>(wn);
+        case 32: return lane_fn_w<32>(wn);
         default: return nullptr;
     }
 }
@@ -1382,93 +1265,123 @@ const void *draw_fn_fw(int fpl, int wpl) {
     }
 }
 
-template <int G, int FPL>
-const void *batch_fn_w(int wpl) {
-    switch (wpl) {
-        case 1: return reinterpret_cast<const void *>(&draw_batch_kernel<G, FPL, 1>);
-        case 2: return reinterpret_cast<const void *>(&draw_batch_kernel<G, FPL, 2>);
-        case 4: return reinterpret_cast<const void *>(&draw_batch_kernel<G, FPL, 4>);
-        case 8: return reinterpret_cast<const void *>(&draw_batch_kernel<G, FPL, 8>);
-        default: return nullptr;
-    }
-}
-
-template <int G>
-const void *batch_fn(int fpl, int wpl) {
-    switch (fpl) {
-        case 1: return batch_fn_w<G, 1>(wpl);
-        case 2: return batch_fn_w<G, 2>(wpl);
-        case 4: return batch_fn_w<G, 4>(wpl);
-        case 8: if constexpr (G == 4) return batch_fn_w<G, 8>(wpl); else return nullptr;
-        default: return nullptr;
-    }
-}
-
 int pow2_ceil_int(int x) {
     int p = 1;
     while (p < x) p <<= 1;
     return p;
 }
 
-// Batch draws: draw_lane_kernel with G = 2 lanes per panel (32 panels per wavefront) when the
-// instance fits (F <= 32, W <= 32, no max = 0 < min feature), else draw_kernel with G = 16
-// (F <= 64) or 64.  draw_batch_kernel (G = 4 / 8) stays selectable.
-// CSA_DRAW_GROUP=4|8|16|64 overrides (benchmarking).  Pick-order / single-attempt draws
-// (general mode) use the G = 64 draw_kernel.
+// Batch draws: draw_lane_kernel (2 lanes per panel, 32 panels per wavefront) when the instance
+// fits -- F <= 32, W <= 32, no max = 0 < min feature, |min|, |selected| < 2^15 (16-bit packed
+// need / remaining) and no feature starting above max ("selected == max" is tested as
+// need <= min - max) -- else draw_kernel with G = 16 (F <= 64, W <= 256) or 64.  Pick-order /
+// single-attempt draws (general mode) use draw_kernel<64, ..., true>.  CSA_DRAW_KERNEL=lane|16|64
+// forces a batch kernel the instance fits (parity tests of every layout).
 int pick_draw_config(const csa_instance *I, bool general, DrawConfig &c) {
-    const bool small = I->F <= 32 && I->d_pmask && !I->zero_max_min && I->n <= 16384;
-    int G = general ? 64 : (small && I->W <= 32) ? 4 : (I->F <= 64 && I->W <= 256) ? 16 : 64;
-    if (const char *e = getenv("CSA_DRAW_GROUP")) {
-        const int g = atoi(e);
-        if (!general && (g == 16 || g == 64 || (small && (g == 4 || g == 8)) || (small && g == 1 && I->W <= 32)))
-            G = g;
+    const bool lane_ok = I->F <= 32 && I->d_pmask && !I->zero_max_min && I->W <= 32 && I->max_abs < 32768 &&
+                         !I->sel_over_max;
+    const bool g16_ok = I->F <= 64 && I->W <= 256;
+    int choice = general ? 64 : lane_ok ? 2 : g16_ok ? 16 : 64;
+    if (const char *e = getenv("CSA_DRAW_KERNEL")) {
+        if (!general && !strcmp(e, "lane") && lane_ok) choice = 2;
+        else if (!general && !strcmp(e, "16") && g16_ok) choice = 16;
+        else if (!general && !strcmp(e, "64")) choice = 64;
     }
-    // draw_lane_kernel group size: 2 lanes per panel by default (fastest at sf_e: 6.06 ms / 10^6
-    // panels vs 7.47 for G = 1 and draw_batch_kernel<4>, 6.30 for G = 4); CSA_DRAW_GROUP=4|8|16|64
-    // selects the other kernels, CSA_DRAW_GROUP=1 / CSA_DRAW_LANE=1|2|4 the lane kernel's G
-    int lane_g = 2;
-    if (const char *e = getenv("CSA_DRAW_GROUP")) lane_g = atoi(e) == 1 ? 1 : 0;
-    if (const char *e = getenv("CSA_DRAW_LANE")) lane_g = atoi(e);
-    // the lane kernel packs need and remaining as 16-bit halves: |min|, |selected| < 2^15 (n <= 16384)
-    // and tests "selected == max" as need <= min - max (selected never starts above max)
-    if (!general && small && I->W <= 32 && I->max_abs < 32768 && !I->sel_over_max &&
-        (lane_g == 1 || lane_g == 2 || lane_g == 4)) {
-        // draw_lane_kernel: FN in {8, 16, 32} (FN / G >= 4), WN in {4, 8, 16, 28, 32}
-        c.G = lane_g;
+    c.G = choice;
+    if (choice == 2) {
         c.lane = true;
-        c.batch = false;
-        c.FPL = std::max({8, 4 * lane_g, pow2_ceil_int(I->F)});
+        c.FPL = std::max(8, pow2_ceil_int(I->F));
         c.WPL = I->W <= 4 ? 4 : I->W <= 8 ? 8 : I->W <= 16 ? 16 : I->W <= 28 ? 28 : 32;
-        c.fn = lane_fn(lane_g, c.FPL, c.WPL);
-        if (!c.fn) return fail(CSA_E_UNSUPPORTED, "no lane draw kernel for G=%d F=%d W=%d", lane_g, I->F, I->W);
+        c.fn = lane_fn(c.FPL, c.WPL);
+        if (!c.fn) return fail(CSA_E_UNSUPPORTED, "no lane draw kernel for F=%d W=%d", I->F, I->W);
         return CSA_OK;
     }
-    c.G = G;
-    c.batch = G <= 8;
-    c.FPL = pow2_ceil_int((I->F + G - 1) / G);
-    c.WPL = pow2_ceil_int(std::max(1, (I->W + G - 1) / G));
+    c.FPL = pow2_ceil_int((I->F + c.G - 1) / c.G);
+    c.WPL = pow2_ceil_int(std::max(1, (I->W + c.G - 1) / c.G));
     if (general)
         c.fn = draw_fn_fw<64, true>(c.FPL, c.WPL);
-    else if (G == 4)
-        c.fn = batch_fn<4>(c.FPL, c.WPL);
-    else if (G == 8)
-        c.fn = batch_fn<8>(c.FPL, c.WPL);
     else
-        c.fn = G == 16 ? draw_fn_fw<16, false>(c.FPL, c.WPL) : draw_fn_fw<64, false>(c.FPL, c.WPL);
+        c.fn = c.G == 16 ? draw_fn_fw<16, false>(c.FPL, c.WPL) : draw_fn_fw<64, false>(c.FPL, c.WPL);
     if (!c.fn)
-        return fail(CSA_E_UNSUPPORTED, "no draw kernel for F=%d n=%d (G=%d needs FPL=%d WPL=%d)", I->F, I->n, G,
+        return fail(CSA_E_UNSUPPORTED, "no draw kernel for F=%d n=%d (G=%d needs FPL=%d WPL=%d)", I->F, I->n, c.G,
                     c.FPL, c.WPL);
     return CSA_OK;
 }
 
+// k = 0 (legacy.py:184 loops zero times): every attempt returns the empty panel, accepted iff no
+// feature is below its minimum (check_min_cats); otherwise the reference restarts forever.
+__global__ void empty_panels_kernel(uint64_t n_panels, uint32_t *attempts, uint32_t *status, uint64_t panel_begin,
+                                    int rejected) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n_panels) return;
+    if (rejected) {
+        if (i == 0) raise_status(status, CSA_E_ATTEMPT_LIMIT, panel_begin);
+    } else if (attempts) {
+        attempts[i] = 1u;
+    }
+}
+
+// per-instance pick-list scratch of the lane kernel, serialised across calls: a draw on any stream
+// waits until the previous draw's picks_pack_kernel has consumed the lists
+int lane_picks(csa_instance *I, uint64_t count, hipStream_t st, uint16_t **out) {
+    if (!I->picks_done) HIPCHK(hipEventCreateWithFlags(&I->picks_done, hipEventDisableTiming));
+    if (I->picks_pending) HIPCHK(hipStreamWaitEvent(st, I->picks_done, 0));
+    const size_t bytes = std::max<uint64_t>(count, 1) * sizeof(uint16_t);
+    if (I->picks_bytes < bytes) {
+        if (I->picks_pending) HIPCHK(hipEventSynchronize(I->picks_done));
+        if (I->d_picks16) HIPCHK(hipFree(I->d_picks16));
+        I->d_picks16 = nullptr;
+        I->picks_bytes = 0;
+        HIPCHK(hipMalloc(reinterpret_cast<void **>(&I->d_picks16), bytes));
+        I->picks_bytes = bytes;
+    }
+    *out = I->d_picks16;
+    return CSA_OK;
+}
+
+int launch_pack(const uint16_t *d_picks, uint64_t n_panels, int k, int W, uint64_t *d_panels, uint64_t *d_hashes,
+                hipStream_t stream) {
+    if (n_panels == 0) return CSA_OK;
+    const int wpb = W <= 16 ? 4 : W <= 64 ? 2 : 1;  // waves (64 panels each) per workgroup: <= 130 KB of LDS
+    const uint64_t blocks = (n_panels + 64 * wpb - 1) / (64 * wpb);
+    const size_t plds = (size_t)wpb * 64 * (2 * W + 1) * 4;
+    hipLaunchKernelGGL(picks_pack_kernel, dim3((unsigned)blocks), dim3(64 * wpb), plds, stream, d_picks, n_panels, k,
+                       W, d_panels, d_hashes);
+    HIPCHK(hipGetLastError());
+    return CSA_OK;
+}
+
+// d_picks_ext: the lane kernel's pick lists go to this caller buffer and are NOT packed (the caller
+// runs csa_picks_pack_async); otherwise to the instance scratch, packed here into d_panels
 int launch_draw(const csa_instance *I, int32_t k, uint64_t seed, uint64_t panel_begin, uint64_t n_panels,
                 uint32_t max_attempts, uint32_t attempt_base, int single, uint64_t *d_panels,
                 uint64_t *d_hashes, uint32_t *d_attempts, int32_t *d_picks, uint32_t *d_status,
-                int32_t *d_sel_out, int32_t *d_rem_out, uint64_t *d_present_out, hipStream_t stream) {
+                int32_t *d_sel_out, int32_t *d_rem_out, uint64_t *d_present_out, hipStream_t stream,
+                uint16_t *d_picks_ext = nullptr) {
     int rc = check_k(I, k);
     if (rc) return rc;
-    if (!d_panels || !d_status) return fail(CSA_E_INVALID, "d_panels and d_status are required");
+    if ((!d_panels && !d_picks_ext) || !d_status) return fail(CSA_E_INVALID, "d_panels and d_status are required");
     if (n_panels == 0) return CSA_OK;
+    if (k == 0 && !single && !d_sel_out && !d_present_out) {
+        int rejected = 0;
+        for (int f = 0; f < I->F; ++f) rejected |= I->sel0[f] < I->fmin[f];
+        if (!d_panels) {  // pick-list draw of k = 0: nothing to write but the attempts / status
+            hipLaunchKernelGGL(empty_panels_kernel, dim3((unsigned)((n_panels + 255) / 256)), dim3(256), 0, stream,
+                               n_panels, d_attempts, d_status, panel_begin, rejected);
+            HIPCHK(hipGetLastError());
+            return CSA_OK;
+        }
+        HIPCHK(hipMemsetAsync(d_panels, 0, n_panels * I->W * 8, stream));
+        hipLaunchKernelGGL(empty_panels_kernel, dim3((unsigned)((n_panels + 255) / 256)), dim3(256), 0, stream,
+                           n_panels, d_attempts, d_status, panel_begin, rejected);
+        HIPCHK(hipGetLastError());
+        if (d_hashes) {
+            hipLaunchKernelGGL(panel_hash_kernel, dim3((unsigned)((n_panels * 4 + 255) / 256)), dim3(256), 0, stream,
+                               d_panels, n_panels, I->W, d_hashes);
+            HIPCHK(hipGetLastError());
+        }
+        return CSA_OK;
+    }
     DrawConfig cfg;
     int rc2 = pick_draw_config(I, single || d_picks || d_sel_out || d_present_out, cfg);
     if (rc2) return rc2;
@@ -1495,35 +1408,40 @@ int launch_draw(const csa_instance *I, int32_t k, uint64_t seed, uint64_t panel_
     A.hashes = d_hashes;
     A.attempts = d_attempts;
     A.picks = d_picks;
+    A.picks16 = nullptr;
     A.status = d_status;
     A.sel_out = d_sel_out;
     A.rem_out = d_rem_out;
     A.present_out = d_present_out;
-    const int threads = cfg.lane ? kLaneThreads : cfg.batch ? kBatchThreads : draw_threads(cfg.FPL, cfg.WPL);
+    if (d_picks_ext && !cfg.lane) return fail(CSA_E_UNSUPPORTED, "this instance does not take the pick-list draw");
+    csa_instance *M = const_cast<csa_instance *>(I);  // the lane kernel's pick-list scratch
+    if (d_picks_ext)
+        A.picks16 = d_picks_ext;
+    else if (cfg.lane && (rc = lane_picks(M, n_panels * (uint64_t)k, stream, &A.picks16)))
+        return rc;
+    const int threads = cfg.lane ? kLaneThreads : draw_threads(cfg.FPL, cfg.WPL);
     const int groups_wg = threads / cfg.G;
-    const size_t lds = cfg.lane    ? lane_lds_bytes(cfg.G, cfg.FPL, cfg.WPL, I->n)
-                       : cfg.batch ? batch_lds_bytes(cfg.G, cfg.FPL, cfg.WPL, I->n, I->W, k, groups_wg)
-                                   : draw_lds_bytes(cfg.G, cfg.FPL, cfg.WPL, I->W, k, groups_wg);
+    const size_t lds = cfg.lane ? lane_lds_bytes(cfg.FPL, cfg.WPL, I->n)
+                                : draw_lds_bytes(cfg.G, cfg.FPL, cfg.WPL, I->W, k, groups_wg);
     if (lds > 160 * 1024) return fail(CSA_E_UNSUPPORTED, "draw kernel needs %zu B of LDS", lds);
-    int per_cu = 0, cus = 0;
-    HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, cfg.fn, threads, lds));
-    HIPCHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, I->device));
     const uint64_t want = (n_panels + groups_wg - 1) / groups_wg;
-    uint64_t cap = (uint64_t)std::max(per_cu, 1) * (uint64_t)std::max(cus, 1);
-    // CSA_DRAW_WAVES=m: m resident grids' worth of workgroups; 0 = one workgroup per 128 panels (not
-    // persistent).  Default: 0 for the lane kernel -- sf_e 10^6 panels: 4.47 ms vs 5.05 ms persistent,
-    // and retiring workgroups let a concurrent stream's kernels in -- 1 (persistent) for the others
-    long waves = cfg.lane ? 0 : 1;
-    if (const char *e = getenv("CSA_DRAW_WAVES")) waves = atol(e);
-    cap = waves <= 0 ? want : cap * (uint64_t)waves;
-    const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min(want, cap));
+    // the lane kernel: one workgroup per 128 panels, not persistent -- sf_e 10^6 panels: 4.47 ms vs
+    // 5.05 ms for a persistent grid, and retiring workgroups let a concurrent stream's kernels in.
+    // draw_kernel: one resident grid (its 66 KB of feature rows at n = 8192 load once per workgroup)
+    uint64_t grid = want;
+    if (!cfg.lane) {
+        int per_cu = 0, cus = 0;
+        HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, cfg.fn, threads, lds));
+        HIPCHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, I->device));
+        grid = std::min(want, (uint64_t)std::max(per_cu, 1) * (uint64_t)std::max(cus, 1));
+    }
     void *args[] = {&A};
-    HIPCHK(hipLaunchKernel(cfg.fn, dim3(grid), dim3(threads), args, lds, stream));
+    HIPCHK(hipLaunchKernel(cfg.fn, dim3((unsigned)std::max<uint64_t>(1, grid)), dim3(threads), args, lds, stream));
     HIPCHK(hipGetLastError());
-    if ((cfg.batch || cfg.lane) && d_hashes) {  // batch / lane kernels leave hashing to a streaming pass
-        hipLaunchKernelGGL(panel_hash_kernel, dim3((unsigned)((n_panels * 4 + 255) / 256)), dim3(256), 0, stream,
-                           d_panels, n_panels, I->W, d_hashes);
-        HIPCHK(hipGetLastError());
+    if (cfg.lane && !d_picks_ext) {  // pick lists -> packed panels (+ hashes)
+        if ((rc = launch_pack(A.picks16, n_panels, k, I->W, d_panels, d_hashes, stream))) return rc;
+        HIPCHK(hipEventRecord(M->picks_done, stream));
+        M->picks_pending = true;
     }
     return CSA_OK;
 }
@@ -1536,6 +1454,8 @@ int read_status(const uint32_t *d_status, hipStream_t stream, uint32_t *h) {
 
 // csa_legacy_sample's pipeline chunk (panels): 2^20 = one bench step at sf_e
 constexpr uint64_t kSampleChunk = 1ull << 20;
+constexpr int kSampleSlot0 = 8, kScratchSlots = 16;          // instance scratch slots of csa_legacy_sample
+constexpr size_t kSampleKeepBytes = (size_t)8 << 30;          // kept across calls up to 8 GiB
 
 uint64_t pow2_at_least(uint64_t x) {
     uint64_t p = 1;
@@ -1603,6 +1523,7 @@ int csa_instance_create(int32_t n, int32_t C, int32_t F, const int32_t *person_f
     I->fmax.assign(fmax, fmax + F);
     I->fcat.assign(feat_cat, feat_cat + F);
     I->pool.assign(F, 0);
+    I->sel0.assign(F, 0);
     I->featmask.assign((size_t)F * I->Ws, 0ull);
     for (int f = 1; f < F; ++f)
         if (feat_cat[f] < feat_cat[f - 1]) {
@@ -1670,9 +1591,17 @@ void csa_instance_destroy(csa_instance *I) {
     if (I->d_rem0) (void)hipFree(I->d_rem0);
     if (I->d_present0) (void)hipFree(I->d_present0);
     if (I->d_pmask) (void)hipFree(I->d_pmask);
-    for (int i = 0; i < 8; ++i)
+    if (I->sdraw) (void)hipStreamSynchronize(I->sdraw);
+    if (I->spost) (void)hipStreamSynchronize(I->spost);
+    for (int i = 0; i < 16; ++i)
         if (I->scratch[i]) (void)hipFree(I->scratch[i]);
     if (I->stream) (void)hipStreamDestroy(I->stream);
+    if (I->sdraw) (void)hipStreamDestroy(I->sdraw);
+    if (I->spost) (void)hipStreamDestroy(I->spost);
+    if (I->drawn) (void)hipEventDestroy(I->drawn);
+    if (I->picks_done) (void)hipEventSynchronize(I->picks_done);
+    if (I->d_picks16) (void)hipFree(I->d_picks16);
+    if (I->picks_done) (void)hipEventDestroy(I->picks_done);
     delete I;
 }
 
@@ -1704,6 +1633,7 @@ int csa_instance_set_state(csa_instance *I, const int32_t *sel, const int32_t *r
         for (int w = 0; w < I->W; ++w)
             if (present[w] & ~all[w]) return fail(CSA_E_INVALID, "present mask has bits beyond n");
     HIPCHK(hipMemcpy(I->d_sel0, sel ? sel : zeros.data(), I->F * 4, hipMemcpyHostToDevice));
+    I->sel0.assign(sel ? sel : zeros.data(), (sel ? sel : zeros.data()) + I->F);
     HIPCHK(hipMemcpy(I->d_rem0, rem ? rem : I->pool.data(), I->F * 4, hipMemcpyHostToDevice));
     if (I->W) HIPCHK(hipMemcpy(I->d_present0, present ? present : all.data(), I->W * 8, hipMemcpyHostToDevice));
     return CSA_OK;
@@ -1730,9 +1660,11 @@ int csa_pair_histogram_async(const int64_t *d_pairs, int32_t n, uint64_t *d_hist
     return CSA_OK;
 }
 
-int csa_hash_buckets_async(const uint64_t *d_hashes, uint64_t n_hashes, uint32_t world, uint64_t *d_out,
-                           uint64_t *d_counts, uint64_t *d_cursor, void *stream) {
-    if (!d_hashes || !d_out || !d_counts || !d_cursor || world == 0 || world > (uint32_t)kMaxWorld)
+int csa_hash_buckets_async(const uint64_t *d_hashes, const uint64_t *d_panels, uint64_t n_hashes, int32_t W,
+                           uint32_t world, uint64_t *d_out, uint64_t *d_out_panels, uint64_t *d_counts,
+                           uint64_t *d_cursor, void *stream) {
+    if (!d_hashes || !d_out || !d_counts || !d_cursor || world == 0 || world > (uint32_t)kMaxWorld ||
+        (d_panels && (!d_out_panels || W <= 0)))
         return fail(CSA_E_INVALID, "hash buckets: bad arguments");
     hipStream_t st = (hipStream_t)stream;
     HIPCHK(hipMemsetAsync(d_counts, 0, (size_t)world * 8, st));
@@ -1748,8 +1680,8 @@ int csa_hash_buckets_async(const uint64_t *d_hashes, uint64_t n_hashes, uint32_t
     HIPCHK(hipGetLastError());
     if (n_hashes) {
         const unsigned grid = (unsigned)std::min<uint64_t>((n_hashes + 255) / 256, 2048);
-        hipLaunchKernelGGL(hash_owner_scatter_kernel, dim3(grid), dim3(256), 0, st, d_hashes, n_hashes, world,
-                           reinterpret_cast<unsigned long long *>(d_cursor), d_out);
+        hipLaunchKernelGGL(hash_owner_scatter_kernel, dim3(grid), dim3(256), 0, st, d_hashes, d_panels, n_hashes, W,
+                           world, reinterpret_cast<unsigned long long *>(d_cursor), d_out, d_out_panels);
         HIPCHK(hipGetLastError());
     }
     return CSA_OK;
@@ -1795,6 +1727,29 @@ int csa_draw_async(const csa_instance *I, int32_t k, uint64_t seed, uint64_t pan
                        d_picks, d_status, nullptr, nullptr, nullptr, (hipStream_t)stream);
 }
 
+int csa_draw_picks_supported(const csa_instance *I, int32_t k) {
+    if (!I || check_k(I, k)) return 0;
+    DrawConfig cfg;
+    return pick_draw_config(I, false, cfg) == CSA_OK && cfg.lane ? 1 : 0;
+}
+
+int csa_draw_picks_async(const csa_instance *I, int32_t k, uint64_t seed, uint64_t panel_begin, uint64_t n_panels,
+                         uint32_t max_attempts, uint16_t *d_picks, uint32_t *d_attempts, uint32_t *d_status,
+                         void *stream) {
+    if (!I || !d_picks) return fail(CSA_E_INVALID, "draw_picks: null instance or d_picks");
+    return launch_draw(I, k, seed, panel_begin, n_panels, max_attempts, 0, 0, nullptr, nullptr, d_attempts, nullptr,
+                       d_status, nullptr, nullptr, nullptr, (hipStream_t)stream, d_picks);
+}
+
+int csa_picks_pack_async(const uint16_t *d_picks, uint64_t n_panels, int32_t k, int32_t n, uint64_t *d_panels,
+                         uint64_t *d_hashes, void *stream) {
+    if (n <= 0 || n > 65536 || k < 0 || (k > 0 && !d_picks) || !d_panels)
+        return fail(CSA_E_INVALID, "picks_pack: bad arguments");
+    const int W = (n + 63) / 64;
+    if ((size_t)64 * (2 * W + 1) * 4 > 160 * 1024) return fail(CSA_E_UNSUPPORTED, "picks_pack: n=%d too large", n);
+    return launch_pack(d_picks, n_panels, k, W, d_panels, d_hashes, (hipStream_t)stream);
+}
+
 int csa_panel_hash_async(const uint64_t *d_panels, uint64_t n_panels, int32_t W, uint64_t *d_hashes,
                          void *stream) {
     if (W <= 0 || !d_panels || !d_hashes) return fail(CSA_E_INVALID, "panel hash: bad arguments");
@@ -1813,10 +1768,10 @@ int csa_draw_kernel_name(const csa_instance *I, int32_t k, char *buf, uint64_t l
     rc = pick_draw_config(I, false, cfg);
     if (rc) return rc;
     if (cfg.lane)
-        snprintf(buf, (size_t)len, "draw_lane_kernel<%d, %d, %d>", cfg.G, cfg.FPL, cfg.WPL);
+        snprintf(buf, (size_t)len, "draw_lane_kernel<%d, %d, %d>", cfg.FPL, cfg.WPL,
+                 (cfg.WPL / 2 + CSA_LANE_SKDIV - 1) / CSA_LANE_SKDIV);
     else
-        snprintf(buf, (size_t)len, "%s<%d, %d, %d%s>", cfg.batch ? "draw_batch_kernel" : "draw_kernel", cfg.G,
-                 cfg.FPL, cfg.WPL, cfg.batch ? "" : ", false");
+        snprintf(buf, (size_t)len, "draw_kernel<%d, %d, %d, false>", cfg.G, cfg.FPL, cfg.WPL);
     return CSA_OK;
 }
 
@@ -1839,7 +1794,7 @@ int csa_transpose_count_async(const uint64_t *d_panels, uint64_t n_panels, int32
 
 namespace {
 struct PairPlan {
-    int npad, nbt, ntri, nsplit, xcd_map;
+    int npad, nbt, ntri, nsplit;
 };
 
 // one 512-thread workgroup per CU (two waves per SIMD): fill the CUs once, keep >= 8 panel
@@ -1857,18 +1812,6 @@ int pair_plan(int32_t n, uint64_t n_blocks, uint32_t engine, PairPlan &p) {
     const uint64_t exact_blocks = engine == CSA_PAIR_FP4 ? (1ull << 24) / 64 : (1ull << 31) / 64;
     ns = std::max<uint64_t>(ns, (n_blocks + exact_blocks - 1) / exact_blocks);
     if (ns > (1u << 20)) return fail(CSA_E_UNSUPPORTED, "pairs: too many panel blocks per call");
-    // XCD-aware split mapping (pair_mfma_kernel; CSA_PAIR_XCD=1) when there are >= 8 splits: round
-    // down to a multiple of 8 unless that breaks the exactness bound.  Off by default: at sf_e it
-    // leaves 32 CUs idle (224 workgroups) and measured 0.90 vs 0.82 ms.
-    p.xcd_map = 0;
-    const char *ex = getenv("CSA_PAIR_XCD");
-    if (ns >= 8 && ex && atoi(ex) == 1) {
-        const uint64_t ns8 = ns / 8 * 8;
-        if (ns8 * exact_blocks >= n_blocks) {
-            ns = ns8;
-            p.xcd_map = 1;
-        }
-    }
     p.nsplit = (int)ns;
     return CSA_OK;
 }
@@ -1898,34 +1841,15 @@ int csa_pair_counts_ex_async(const uint64_t *d_xt, uint64_t n_blocks, int32_t n,
                     (unsigned long long)scratch_bytes, (unsigned long long)csa_pair_scratch_bytes(n, n_blocks, engine));
     const dim3 grid(p.ntri * p.nsplit), block(kPairThreads);
     int32_t *part = static_cast<int32_t *>(d_scratch);
-    // panel blocks staged per barrier (prefetch distance): CSA_PAIR_KB = 4 / 8 / 16 overrides
-    int kb = kPairKB;
-    if (const char *e = getenv("CSA_PAIR_KB")) kb = atoi(e);
-    const void *fn = nullptr;
-#define CSA_PAIR_FN(F4, PA)                                                                       \
-    (kb == 16 ? reinterpret_cast<const void *>(&pair_mfma_kernel<F4, PA, 16>)                     \
-              : kb == 8 ? reinterpret_cast<const void *>(&pair_mfma_kernel<F4, PA, 8>)            \
-                        : reinterpret_cast<const void *>(&pair_mfma_kernel<F4, PA, 4>))
-    // fp4 engine, CSA_PAIR_WIDE=1: the wide kernel (4 waves of 128 x 128, one wave per SIMD).
-    // Off by default: 0.71 vs 0.64 ms at sf_e -- one wave per SIMD hides the LDS/VALU latency worse
-    bool wide = false;
-    if (const char *e = getenv("CSA_PAIR_WIDE")) wide = engine == CSA_PAIR_FP4 && atoi(e) != 0;
-    if (wide)
-        fn = kb == 16 ? (partial ? reinterpret_cast<const void *>(&pair_mfma_wide_kernel<true, 16>)
-                                 : reinterpret_cast<const void *>(&pair_mfma_wide_kernel<false, 16>))
-             : kb == 4 ? (partial ? reinterpret_cast<const void *>(&pair_mfma_wide_kernel<true, 4>)
-                                  : reinterpret_cast<const void *>(&pair_mfma_wide_kernel<false, 4>))
-                       : (partial ? reinterpret_cast<const void *>(&pair_mfma_wide_kernel<true, 8>)
-                                  : reinterpret_cast<const void *>(&pair_mfma_wide_kernel<false, 8>));
-    else if (engine == CSA_PAIR_FP4)
-        fn = partial ? CSA_PAIR_FN(true, true) : CSA_PAIR_FN(true, false);
-    else
-        fn = partial ? CSA_PAIR_FN(false, true) : CSA_PAIR_FN(false, false);
-#undef CSA_PAIR_FN
+    const void *fn = engine == CSA_PAIR_FP4
+                         ? (partial ? reinterpret_cast<const void *>(&pair_mfma_kernel<true, true, kPairKB>)
+                                    : reinterpret_cast<const void *>(&pair_mfma_kernel<true, false, kPairKB>))
+                         : (partial ? reinterpret_cast<const void *>(&pair_mfma_kernel<false, true, kPairKB>)
+                                    : reinterpret_cast<const void *>(&pair_mfma_kernel<false, false, kPairKB>));
     uint64_t nb = n_blocks;
-    int npad = p.npad, nbt = p.nbt, nsplit = p.nsplit, xcd = p.xcd_map;
-    void *args[] = {(void *)&d_xt, &nb, &n, &npad, &nbt, &nsplit, &d_pairs, &part, &xcd};
-    HIPCHK(hipLaunchKernel(fn, grid, wide ? dim3(256) : block, args, 0, st));
+    int npad = p.npad, nbt = p.nbt, nsplit = p.nsplit;
+    void *args[] = {(void *)&d_xt, &nb, &n, &npad, &nbt, &nsplit, &d_pairs, &part};
+    HIPCHK(hipLaunchKernel(fn, grid, block, args, 0, st));
     HIPCHK(hipGetLastError());
     if (partial) {
         hipLaunchKernelGGL(pair_reduce_kernel, dim3(kPairBlock, p.ntri), dim3(256), 0, st, part, n, p.nbt, p.nsplit,
@@ -1940,8 +1864,8 @@ int csa_pair_counts_async(const uint64_t *d_xt, uint64_t n_blocks, int32_t n, in
 }
 
 int csa_unique_async(const uint64_t *d_hashes, const uint64_t *d_panels, uint64_t n_panels, int32_t W,
-                     uint64_t *d_table, uint64_t table_slots, uint64_t *d_unique, void *stream) {
-    if (!d_hashes || !d_table || !d_unique || W <= 0) return fail(CSA_E_INVALID, "unique: bad arguments");
+                     uint64_t *d_table, uint64_t table_slots, uint64_t *d_unique, uint32_t *d_status, void *stream) {
+    if (!d_hashes || !d_panels || !d_table || !d_unique || W <= 0) return fail(CSA_E_INVALID, "unique: bad arguments");
     if (table_slots < 2 * n_panels || (table_slots & (table_slots - 1)))
         return fail(CSA_E_INVALID, "unique: table_slots must be a power of two >= 2*n_panels");
     if (n_panels == 0) return CSA_OK;
@@ -1951,7 +1875,9 @@ int csa_unique_async(const uint64_t *d_hashes, const uint64_t *d_panels, uint64_
     while ((1ull << pbits) * 1024 < n_panels && pbits < 13) ++pbits;
     const uint64_t P = 1ull << pbits;
     const char *ue = getenv("CSA_UNIQUE_PART");
-    const bool part = d_panels && n_panels >= 65536 && n_panels < (1ull << 31) && n_panels / P <= 2048 &&
+    // (its per-partition LDS tables report an overflow through d_status: without one, the
+    // single-table path, which cannot overflow, runs)
+    const bool part = d_status && n_panels >= 65536 && n_panels < (1ull << 31) && n_panels / P <= 2048 &&
                       !(ue && atoi(ue) == 0);
     if (part) {
         const uint64_t CH = std::max<uint64_t>(4096, ((n_panels + 1023) / 1024 + 255) / 256 * 256);
@@ -1967,7 +1893,7 @@ int csa_unique_async(const uint64_t *d_hashes, const uint64_t *d_panels, uint64_
             hipLaunchKernelGGL(uq_scatter_kernel, dim3(nwg), dim3(kUqThreads), 0, st, d_hashes, n_panels, CH, pbits,
                                nwg, hist, pbase, idx);
             hipLaunchKernelGGL(uq_dedupe_kernel, dim3((unsigned)P), dim3(kUqThreads), 0, st, d_hashes, d_panels, W,
-                               idx, pbase, reinterpret_cast<unsigned long long *>(d_unique));
+                               idx, pbase, reinterpret_cast<unsigned long long *>(d_unique), d_status);
             HIPCHK(hipGetLastError());
             return CSA_OK;
         }
@@ -1976,23 +1902,7 @@ int csa_unique_async(const uint64_t *d_hashes, const uint64_t *d_panels, uint64_
     const unsigned grid = (unsigned)((n_panels + 255) / 256);
     hipLaunchKernelGGL(unique_kernel, dim3(grid), dim3(256), 0, st, d_hashes, d_panels, n_panels, W,
                        reinterpret_cast<unsigned long long *>(d_table), table_slots - 1,
-                       reinterpret_cast<unsigned long long *>(d_unique), 1u, 0u);
-    HIPCHK(hipGetLastError());
-    return CSA_OK;
-}
-
-int csa_unique_hashes_async(const uint64_t *d_hashes, uint64_t n_hashes, uint32_t world, uint32_t rank,
-                            uint64_t *d_table, uint64_t table_slots, uint64_t *d_unique, void *stream) {
-    if (!d_hashes || !d_table || !d_unique || world == 0 || rank >= world)
-        return fail(CSA_E_INVALID, "unique_hashes: bad arguments");
-    if (table_slots < 2 * n_hashes || (table_slots & (table_slots - 1)))
-        return fail(CSA_E_INVALID, "unique_hashes: table_slots must be a power of two >= 2*n_hashes");
-    if (n_hashes == 0) return CSA_OK;
-    HIPCHK(hipMemsetAsync(d_table, 0, table_slots * 8, (hipStream_t)stream));
-    const unsigned grid = (unsigned)((n_hashes + 255) / 256);
-    hipLaunchKernelGGL(unique_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, d_hashes, nullptr,
-                       n_hashes, 1, reinterpret_cast<unsigned long long *>(d_table), table_slots - 1,
-                       reinterpret_cast<unsigned long long *>(d_unique), world, rank);
+                       reinterpret_cast<unsigned long long *>(d_unique));
     HIPCHK(hipGetLastError());
     return CSA_OK;
 }
@@ -2020,80 +1930,89 @@ int csa_legacy_sample(csa_instance *I, int32_t k, uint64_t seed, uint64_t panel_
     ScopedDevice sd(I->device);
     const int n = I->n, W = I->W;
     const int npad = csa_xt_pad(std::max(n, 1));
-    // Chunked two-stream pipeline: chunk c + 1 is drawn (stream sd) while chunk c is hashed,
-    // transposed, counted and paired (stream sp); the panels and hashes buffers hold the whole
-    // batch (output copy, exact distinct count at the end), XT and the pair scratch one chunk.
+    // Chunked two-stream pipeline: chunk c + 1 is drawn (stream sd) while chunk c is transposed,
+    // counted and paired (stream sp); the panels and hashes buffers hold the whole batch (output
+    // copy, exact distinct count at the end), XT and the pair scratch one chunk.  Streams, event
+    // and buffers belong to the instance and are reused by the next call (grow-only; a batch
+    // above kSampleKeepBytes of device memory frees its buffers again on return).
     uint64_t chunk = kSampleChunk;
     if (const char *e = getenv("CSA_SAMPLE_CHUNK")) chunk = std::max<uint64_t>(64, strtoull(e, nullptr, 10));
     chunk = std::min(chunk, std::max<uint64_t>(n_panels, 1));
     const uint64_t cblk = (chunk + 63) / 64;
-    DevBuf<uint64_t> panels, hashes, xt, table, uniq;  // freed after the guard below drained the streams
-    DevBuf<int64_t> counts, pairs;
-    DevBuf<uint32_t> attempts, status;
-    DevBuf<int32_t> scratch;
-    hipStream_t sdraw = nullptr, spost = nullptr;
-    hipEvent_t drawn = nullptr;
-    struct Guard {
-        hipStream_t a = nullptr, b = nullptr;
-        hipEvent_t e = nullptr;
-        ~Guard() {  // drain both streams before the buffers below are freed
-            if (a) (void)hipStreamSynchronize(a);
-            if (b) (void)hipStreamSynchronize(b);
-            if (e) (void)hipEventDestroy(e);
-            if (a) (void)hipStreamDestroy(a);
-            if (b) (void)hipStreamDestroy(b);
+    if (!I->sdraw) HIPCHK(hipStreamCreateWithFlags(&I->sdraw, hipStreamNonBlocking));
+    if (!I->spost) HIPCHK(hipStreamCreateWithFlags(&I->spost, hipStreamNonBlocking));
+    if (!I->drawn) HIPCHK(hipEventCreateWithFlags(&I->drawn, hipEventDisableTiming));
+    hipStream_t sdraw = I->sdraw, spost = I->spost;
+    struct Drain {  // every exit leaves both streams idle, so the next call may reuse the buffers
+        csa_instance *I;
+        ~Drain() {
+            (void)hipStreamSynchronize(I->sdraw);
+            (void)hipStreamSynchronize(I->spost);
+            size_t held = 0;
+            for (int j = kSampleSlot0; j < kScratchSlots; ++j) held += I->scratch_bytes[j];
+            if (held > kSampleKeepBytes)
+                for (int j = kSampleSlot0; j < kScratchSlots; ++j)
+                    if (I->scratch[j]) {
+                        (void)hipFree(I->scratch[j]);
+                        I->scratch[j] = nullptr;
+                        I->scratch_bytes[j] = 0;
+                    }
         }
-    } guard;
-    HIPCHK(hipStreamCreateWithFlags(&sdraw, hipStreamNonBlocking));
-    guard.a = sdraw;
-    HIPCHK(hipStreamCreateWithFlags(&spost, hipStreamNonBlocking));
-    guard.b = spost;
-    HIPCHK(hipEventCreateWithFlags(&drawn, hipEventDisableTiming));
-    guard.e = drawn;
+    } drain{I};
     int rc;
     const bool want_unique = flags & CSA_WANT_UNIQUE, want_pairs = flags & CSA_WANT_PAIRS;
     const bool want_counts = flags & CSA_WANT_COUNTS;
     const uint64_t slots = pow2_at_least(std::max<uint64_t>(2 * n_panels, 64));
     const uint64_t sb = want_pairs ? csa_pair_scratch_bytes(n, cblk, CSA_PAIR_FP4) : 0;
-    if ((rc = dalloc(&panels.p, std::max<uint64_t>(n_panels, 1) * W)) || (rc = dalloc(&status.p, 4))) return rc;
-    if (want_unique && ((rc = dalloc(&hashes.p, 2 * std::max<uint64_t>(n_panels, 1))) ||
-                        (rc = dalloc(&table.p, slots)) || (rc = dalloc(&uniq.p, 1))))
+    uint64_t *panels = nullptr, *hashes = nullptr, *xt = nullptr, *table = nullptr, *uniq = nullptr;
+    int64_t *counts = nullptr, *pairs = nullptr;
+    uint32_t *attempts = nullptr, *status = nullptr;
+    int32_t *pscratch = nullptr;
+    int sl = kSampleSlot0;
+    if ((rc = scratch(I, sl++, std::max<uint64_t>(n_panels, 1) * W, &panels)) || (rc = scratch(I, sl++, 4, &status)))
         return rc;
-    if (attempts_out && (rc = dalloc(&attempts.p, std::max<uint64_t>(n_panels, 1)))) return rc;
-    if ((want_counts || want_pairs) && (rc = dalloc(&counts.p, n))) return rc;
-    if (want_pairs && ((rc = dalloc(&xt.p, cblk * npad)) || (rc = dalloc(&pairs.p, (size_t)n * n)) ||
-                       (rc = dalloc(&scratch.p, sb / sizeof(int32_t) + 1))))
+    if (want_unique && ((rc = scratch(I, sl++, 2 * std::max<uint64_t>(n_panels, 1), &hashes)) ||
+                        (rc = scratch(I, sl++, slots, &table)) || (rc = scratch(I, sl++, 1, &uniq))))
         return rc;
-    HIPCHK(hipMemsetAsync(status.p, 0, 16, sdraw));
-    if (counts.p) HIPCHK(hipMemsetAsync(counts.p, 0, (size_t)n * 8, spost));
-    if (pairs.p) HIPCHK(hipMemsetAsync(pairs.p, 0, (size_t)n * n * 8, spost));
-    if (uniq.p) HIPCHK(hipMemsetAsync(uniq.p, 0, 8, spost));
+    if (attempts_out && (rc = scratch(I, sl++, std::max<uint64_t>(n_panels, 1), &attempts))) return rc;
+    if ((want_counts || want_pairs) && (rc = scratch(I, sl++, (size_t)n, &counts))) return rc;
+    if (want_pairs && ((rc = scratch(I, sl++, cblk * npad, &xt)) || (rc = scratch(I, sl++, (size_t)n * n, &pairs)) ||
+                       (rc = scratch(I, sl++, sb / sizeof(int32_t) + 1, &pscratch))))
+        return rc;
+    HIPCHK(hipMemsetAsync(status, 0, 16, sdraw));
+    if (counts) HIPCHK(hipMemsetAsync(counts, 0, (size_t)n * 8, spost));
+    if (uniq) HIPCHK(hipMemsetAsync(uniq, 0, 8, spost));
     for (uint64_t off = 0; off < n_panels; off += chunk) {
         const uint64_t len = std::min(chunk, n_panels - off);
-        uint64_t *cp = panels.p + off * W;
-        if ((rc = launch_draw(I, k, seed, panel_begin + off, len, max_attempts, 0, 0, cp, nullptr,
-                              attempts.p ? attempts.p + off : nullptr, nullptr, status.p, nullptr, nullptr,
-                              nullptr, sdraw)))
+        uint64_t *cp = panels + off * W;
+        // the draw also writes the panels' 128-bit hashes (picks_pack_kernel / draw_kernel)
+        if ((rc = launch_draw(I, k, seed, panel_begin + off, len, max_attempts, 0, 0, cp,
+                              want_unique ? hashes + 2 * off : nullptr, attempts ? attempts + off : nullptr, nullptr,
+                              status, nullptr, nullptr, nullptr, sdraw)))
             return rc;
-        HIPCHK(hipEventRecord(drawn, sdraw));
-        HIPCHK(hipStreamWaitEvent(spost, drawn, 0));
-        if (want_unique && (rc = csa_panel_hash_async(cp, len, W, hashes.p + 2 * off, spost))) return rc;
-        if (counts.p && (rc = csa_transpose_count_async(cp, len, n, xt.p, counts.p, spost))) return rc;
-        if (pairs.p && (rc = csa_pair_counts_ex_async(xt.p, (len + 63) / 64, n, pairs.p, CSA_PAIR_FP4, scratch.p,
-                                                      sb, spost)))
+        HIPCHK(hipEventRecord(I->drawn, sdraw));
+        HIPCHK(hipStreamWaitEvent(spost, I->drawn, 0));
+        if (counts && (rc = csa_transpose_count_async(cp, len, n, xt, counts, spost))) return rc;
+        // the first chunk stores its pair counts (no n*n zero-fill), later chunks add theirs
+        if (pairs && (rc = csa_pair_counts_ex_async(xt, (len + 63) / 64, n, pairs,
+                                                    CSA_PAIR_FP4 | (off == 0 ? CSA_PAIR_OVERWRITE : 0u), pscratch,
+                                                    sb, spost)))
             return rc;
     }
-    uint32_t hs[4];
-    if ((rc = read_status(status.p, sdraw, hs))) return rc;
-    if ((rc = csa_status_decode(hs))) return rc;
-    if (want_unique && (rc = csa_unique_async(hashes.p, panels.p, n_panels, W, table.p, slots, uniq.p, spost)))
+    if (want_pairs && n_panels == 0) HIPCHK(hipMemsetAsync(pairs, 0, (size_t)n * n * 8, spost));
+    HIPCHK(hipEventRecord(I->drawn, sdraw));
+    HIPCHK(hipStreamWaitEvent(spost, I->drawn, 0));
+    if (want_unique && (rc = csa_unique_async(hashes, panels, n_panels, W, table, slots, uniq, status, spost)))
         return rc;
+    uint32_t hs[4];
+    if ((rc = read_status(status, spost, hs))) return rc;
+    if ((rc = csa_status_decode(hs))) return rc;
     if (flags & CSA_WANT_PANELS)
-        HIPCHK(hipMemcpyAsync(panels_out, panels.p, n_panels * W * 8, hipMemcpyDeviceToHost, spost));
-    if (want_counts) HIPCHK(hipMemcpyAsync(person_counts, counts.p, (size_t)n * 8, hipMemcpyDeviceToHost, spost));
-    if (want_pairs) HIPCHK(hipMemcpyAsync(pair_counts, pairs.p, (size_t)n * n * 8, hipMemcpyDeviceToHost, spost));
-    if (want_unique) HIPCHK(hipMemcpyAsync(unique_out, uniq.p, 8, hipMemcpyDeviceToHost, spost));
-    if (attempts_out) HIPCHK(hipMemcpyAsync(attempts_out, attempts.p, n_panels * 4, hipMemcpyDeviceToHost, spost));
+        HIPCHK(hipMemcpyAsync(panels_out, panels, n_panels * W * 8, hipMemcpyDeviceToHost, spost));
+    if (want_counts) HIPCHK(hipMemcpyAsync(person_counts, counts, (size_t)n * 8, hipMemcpyDeviceToHost, spost));
+    if (want_pairs) HIPCHK(hipMemcpyAsync(pair_counts, pairs, (size_t)n * n * 8, hipMemcpyDeviceToHost, spost));
+    if (want_unique) HIPCHK(hipMemcpyAsync(unique_out, uniq, 8, hipMemcpyDeviceToHost, spost));
+    if (attempts_out) HIPCHK(hipMemcpyAsync(attempts_out, attempts, n_panels * 4, hipMemcpyDeviceToHost, spost));
     HIPCHK(hipStreamSynchronize(spost));
     return CSA_OK;
 }
@@ -2125,7 +2044,7 @@ int csa_first_panel_not_in(csa_instance *I, int32_t k, uint64_t seed, uint64_t p
         HIPCHK(hipMemcpyAsync(pport, portfolio, m * W * 8, hipMemcpyHostToDevice, st));
         if ((rc = csa_panel_hash_async(pport, m, W, phash, st))) return rc;
         HIPCHK(hipMemsetAsync(cnt, 0, 8, st));
-        if ((rc = csa_unique_async(phash, pport, m, W, table, slots, cnt, st))) return rc;
+        if ((rc = csa_unique_async(phash, pport, m, W, table, slots, cnt, nullptr, st))) return rc;
     }
     // chunks of growing size: the expected first non-member is near the start
     uint64_t done = 0, len = std::min(chunk, n_panels);
@@ -2133,10 +2052,9 @@ int csa_first_panel_not_in(csa_instance *I, int32_t k, uint64_t seed, uint64_t p
         len = std::min(len, n_panels - done);
         HIPCHK(hipMemsetAsync(status, 0, 16, st));
         HIPCHK(hipMemsetAsync(first, 0xFF, 8, st));
-        if ((rc = launch_draw(I, k, seed, panel_begin + done, len, max_attempts, 0, 0, panels, nullptr, nullptr,
+        if ((rc = launch_draw(I, k, seed, panel_begin + done, len, max_attempts, 0, 0, panels, hashes, nullptr,
                               nullptr, status, nullptr, nullptr, nullptr, st)))
             return rc;
-        if ((rc = csa_panel_hash_async(panels, len, W, hashes, st))) return rc;
         hipLaunchKernelGGL(member_scan_kernel, dim3((unsigned)((len + 255) / 256)), dim3(256), 0, st, hashes,
                            panels, len, W, reinterpret_cast<const unsigned long long *>(table), slots - 1,
                            phash, pport, reinterpret_cast<unsigned long long *>(first));

@@ -4,12 +4,13 @@ PyTorch only provides device memory, the stream and (in distributed.py) the
 RCCL collectives; every kernel is the hand-written HIP in csrc/.  One
 ``run`` = one pass of analysis.py:162-191 over a shard of panels:
 
-    draw_(batch_)kernel  panels [panel_begin, panel_begin+S) -> packed bitmasks
-    panel_hash_kernel  bitmasks -> 128-bit panel hashes                    (if want_unique)
+    draw_lane_kernel   panels [panel_begin, panel_begin+S) -> pick lists       (draw_picks)
+    picks_pack_kernel  pick lists -> packed bitmasks + 128-bit panel hashes    (pack)
+      (instances beyond the lane kernel: draw_kernel writes bitmasks + hashes directly)
     xt_count_kernel    bitmasks -> transposed panel-indicator bits + per-person counts (+=)
     pair_mfma_kernel   transposed bits -> int32 partial blocks of X^T X on fp4 (default) or
-    pair_reduce_kernel   int8 MFMA -> pair counts (+=)                  (if want_pairs)
-    unique_kernel      hashes (+ bitmasks) -> distinct-panel count (+=)  (if want_unique)
+    pair_reduce_kernel   int8 MFMA -> pair counts (+=, or = with overwrite)  (if want_pairs)
+    uq_* kernels       hashes + bitmasks -> exact distinct-panel count (+=) (if want_unique)
 
 Buffers are allocated once for the largest shard and reused across runs, so a
 timed loop measures kernels only.
@@ -48,6 +49,10 @@ class DevicePipeline:
         dev = self.device
         u64 = torch.int64  # raw 64-bit words; reinterpretation is done by the kernels
         with torch.cuda.device(dev):
+            _ = enc.handle  # upload the instance on this device
+            # the lane kernel writes pick lists (u16) that picks_pack_kernel packs; others write bitmasks
+            self.split_draw = bool(L.csa_draw_picks_supported(enc.handle, self.k)) and self.k > 0
+            self.picks = torch.empty(max(S * self.k, 1), dtype=torch.int16, device=dev) if self.split_draw else None
             self.panels = torch.empty(S * W, dtype=u64, device=dev)
             self.hashes = torch.empty(2 * S, dtype=u64, device=dev) if want_unique else None
             self.attempts = torch.empty(S, dtype=torch.int32, device=dev) if want_attempts else None
@@ -59,7 +64,6 @@ class DevicePipeline:
             self.pair_scratch = torch.empty((sb + 3) // 4, dtype=torch.int32, device=dev) if want_pairs else None
             self.table = torch.empty(slots, dtype=u64, device=dev) if want_unique else None
             self.unique = torch.zeros(1, dtype=torch.int64, device=dev)
-        _ = enc.handle  # upload the instance on this device
 
     def reset(self, status=True, pairs=True):
         """Zero the accumulators.  ``pairs=False`` skips the n*n pair matrix for a caller whose next
@@ -73,13 +77,31 @@ class DevicePipeline:
                 self.pairs.zero_()
 
     # individual stages (stream-ordered, no sync) -------------------------------------------
+    def draw_picks(self, seed, panel_begin, S, max_attempts=0, stream=None):
+        """Pick-list draw (draw_lane_kernel) into self.picks; ``pack`` turns it into panels."""
+        assert self.split_draw and S <= self.max_panels
+        N.check(N.lib().csa_draw_picks_async(self.enc.handle, self.k, int(seed) & 0xFFFFFFFFFFFFFFFF,
+                                             int(panel_begin), int(S), max_attempts, N.ptr(self.picks),
+                                             N.ptr(self.attempts), N.ptr(self.status),
+                                             _stream_ptr(stream or self.stream)))
+
+    def pack(self, S, stream=None):
+        """Pick lists -> self.panels (+ self.hashes with want_unique)."""
+        N.check(N.lib().csa_picks_pack_async(N.ptr(self.picks), int(S), self.k, self.enc.n, N.ptr(self.panels),
+                                             N.ptr(self.hashes), _stream_ptr(stream or self.stream)))
+
     def draw(self, seed, panel_begin, S, max_attempts=0, stream=None):
-        """Draw into self.panels on ``stream`` (default: the pipeline's stream).  A caller that
-        overlaps the draw of the next batch with this batch's counting swaps ``self.panels``
-        between two buffers and orders the streams with events (bench.py --overlap)."""
+        """Draw into self.panels (and, with want_unique, their hashes into self.hashes) on
+        ``stream`` (default: the pipeline's stream).  A caller that overlaps the draw of the next
+        batch with this batch's counting swaps ``self.panels`` / ``self.hashes`` between buffers
+        and orders the streams with events (bench.py)."""
         assert S <= self.max_panels and self.panels.numel() >= S * self.enc.W
+        if self.split_draw:
+            self.draw_picks(seed, panel_begin, S, max_attempts, stream)
+            self.pack(S, stream)
+            return
         N.check(N.lib().csa_draw_async(self.enc.handle, self.k, int(seed) & 0xFFFFFFFFFFFFFFFF, int(panel_begin),
-                                       int(S), max_attempts, N.ptr(self.panels), None,
+                                       int(S), max_attempts, N.ptr(self.panels), N.ptr(self.hashes),
                                        N.ptr(self.attempts), None, N.ptr(self.status),
                                        _stream_ptr(stream or self.stream)))
 
@@ -111,17 +133,16 @@ class DevicePipeline:
 
     def unique_count(self, S):
         N.check(N.lib().csa_unique_async(N.ptr(self.hashes), N.ptr(self.panels), int(S), self.enc.W,
-                                         N.ptr(self.table), self.slots, N.ptr(self.unique),
+                                         N.ptr(self.table), self.slots, N.ptr(self.unique), N.ptr(self.status),
                                          _stream_ptr(self.stream)))
 
-    def run(self, seed, panel_begin, S, max_attempts=0):
-        """Enqueue the whole pass; results accumulate into counts / pairs / unique."""
+    def run(self, seed, panel_begin, S, max_attempts=0, overwrite_pairs=False):
+        """Enqueue the whole pass; results accumulate into counts / pairs / unique (pairs are
+        stored instead with ``overwrite_pairs``)."""
         self.draw(seed, panel_begin, S, max_attempts)
-        if self.want_unique:
-            self.hash(S)
         self.transpose_count(S)
         if self.want_pairs:
-            self.pair_counts(S)
+            self.pair_counts(S, overwrite=overwrite_pairs)
         if self.want_unique:
             self.unique_count(S)
 

@@ -11,15 +11,20 @@ Exchange steps (the only collectives on the path):
   * pair counts        all_reduce(SUM) of the upper triangle packed to int32
                        (csa_pairs_pack/unpack_async; int64[n*n] if a count may
                        reach 2^31)
-  * distinct panels    every 128-bit panel hash goes to its OWNER rank
-                       (h1 % world) with one all_to_all (buckets from
-                       csa_hash_buckets_async); the owner counts its distinct
-                       hashes with the device hash table (csa_unique_hashes_async),
-                       then all_reduce(SUM).  Exact within a rank (bitmask compare in
-                       the single-rank path); across ranks two panels merge when
-                       their 128-bit hashes agree (collision odds ~S^2/2^129).
-On CPU (gloo, tests) the same exchange runs on host tensors and the owner
-dedupe uses numpy; ``panel_hashes`` mirrors the device hash for that path.
+  * distinct panels    every panel -- its 128-bit hash AND its W-word bitmask --
+                       goes to its OWNER rank (h1 % world; equal panels have
+                       equal hashes, so all copies of a panel meet at one owner)
+                       with all_to_all (buckets from csa_hash_buckets_async); the
+                       owner counts its distinct panels with csa_unique_async,
+                       which compares bitmasks on a hash match, so the count is
+                       exact (analysis.py:171,186: a set of sorted tuples); then
+                       all_reduce(SUM) of the owners' counts.
+The bucket sizes are negotiated with a small all_to_all whose result the host
+reads (the only host synchronisation of the exchange); bench.py enqueues the
+next steps' draws before it, so the draw stream never waits for it.
+On CPU (gloo, tests) the same exchange runs on host tensors: numpy bucketing by
+owner and an exact numpy dedupe of the bitmasks; ``panel_hashes`` mirrors the
+device hash for that path.
 """
 import ctypes
 import os
@@ -68,7 +73,7 @@ def _fmix_b(z):
 
 
 def panel_hashes(panels):
-    """Host mirror of the draw kernel's 128-bit panel hash: uint64[S, 2] from uint64[S, W]."""
+    """Host mirror of the device 128-bit panel hash: uint64[S, 2] from uint64[S, W]."""
     p = np.ascontiguousarray(panels, np.uint64)
     S, W = p.shape
     w = np.arange(W, dtype=np.uint64)
@@ -78,17 +83,27 @@ def panel_hashes(panels):
     return np.stack([h1, h2], axis=1)
 
 
-def dedupe_hash_partition(all_hashes, world, r):
-    """Number of distinct 128-bit hashes owned by rank r (owner = h1 mod world)."""
-    h = np.asarray(all_hashes, np.uint64).reshape(-1, 2)
-    mine = h[(h[:, 0] % np.uint64(world)) == np.uint64(r)]
-    if len(mine) == 0:
+def owner_buckets(hashes, panels, world):
+    """Host mirror of csa_hash_buckets_async: (hashes, panels, counts) in owner-major order,
+    owner = h1 % world."""
+    h = np.asarray(hashes, np.uint64).reshape(-1, 2)
+    p = np.asarray(panels, np.uint64).reshape(len(h), -1)
+    owner = (h[:, 0] % np.uint64(world)).astype(np.int64)
+    order = np.argsort(owner, kind="stable")
+    return h[order], p[order], np.bincount(owner, minlength=world).astype(np.int64)
+
+
+def distinct_exact(hashes, panels):
+    """Host mirror of csa_unique_async: distinct panels, equal iff hash AND bitmask are equal."""
+    p = np.asarray(panels, np.uint64)
+    if len(p) == 0:
         return 0
-    return int(len(np.unique(mine, axis=0)))
+    h = np.asarray(hashes, np.uint64).reshape(len(p), 2)
+    return int(len(np.unique(np.concatenate([h, p.reshape(len(p), -1)], axis=1), axis=0)))
 
 
 class HashTable:
-    """Reusable device table for csa_unique_hashes_async (grows on demand)."""
+    """Reusable device table + count for csa_unique_async (grows on demand)."""
 
     def __init__(self, max_hashes, device):
         import torch
@@ -108,43 +123,50 @@ class HashTable:
 
 
 def _host_collectives(t):
-    """gloo has no all_to_all for device tensors: rehearsals (CSA_BENCH_BACKEND=gloo) go via host."""
+    """gloo rehearsals of the device path (CSA_BENCH_BACKEND=gloo) run the collectives on host copies."""
     import torch.distributed as dist
     return t.is_cuda and dist.get_backend() != "nccl"
 
 
-def exchange_hashes(hashes, stream=None):
-    """Send every 128-bit panel hash to its owner rank (h1 % world) with one all_to_all.
+def exchange_panels(hashes, panels, W, stream=None):
+    """Send every panel (128-bit hash + W-word bitmask) to its owner rank h1 % world.
 
-    hashes: int64[2*S_local] on the device (buckets from csa_hash_buckets_async) or on the host
-    (numpy bucketing, gloo tests).  Returns int64[2*S_owned], the hashes this rank owns."""
+    hashes: int64[2*S_local], panels: int64[S_local*W], both on the device (buckets from
+    csa_hash_buckets_async) or on the host (numpy bucketing).  Returns (hashes, panels) this rank
+    owns: int64[2*m], int64[m*W]."""
     import torch
     import torch.distributed as dist
     world = dist.get_world_size()
     n = hashes.numel() // 2
     if hashes.is_cuda:
         from . import _native as N
-        out = torch.empty_like(hashes)
+        out_h = torch.empty_like(hashes)
+        out_p = torch.empty(max(n * W, 1), dtype=torch.int64, device=hashes.device)
         counts = torch.empty(world, dtype=torch.int64, device=hashes.device)
         cursor = torch.empty(world, dtype=torch.int64, device=hashes.device)
         sp = ctypes.c_void_p((stream or torch.cuda.current_stream(hashes.device)).cuda_stream)
-        N.check(N.lib().csa_hash_buckets_async(N.ptr(hashes), n, world, N.ptr(out), N.ptr(counts), N.ptr(cursor), sp))
+        N.check(N.lib().csa_hash_buckets_async(N.ptr(hashes), N.ptr(panels), n, W, world, N.ptr(out_h),
+                                               N.ptr(out_p), N.ptr(counts), N.ptr(cursor), sp))
+        out_p = out_p[: n * W]
     else:
-        h = hashes.numpy().view(np.uint64).reshape(-1, 2)
-        owner = (h[:, 0] % np.uint64(world)).astype(np.int64)
-        order = np.argsort(owner, kind="stable")
-        out = torch.from_numpy(np.ascontiguousarray(h[order]).view(np.int64).reshape(-1))
-        counts = torch.from_numpy(np.bincount(owner, minlength=world).astype(np.int64))
-    via_host = _host_collectives(out)
+        h, p, c = owner_buckets(hashes.numpy().view(np.uint64), panels.numpy().view(np.uint64).reshape(n, W), world)
+        out_h = torch.from_numpy(np.ascontiguousarray(h).view(np.int64).reshape(-1))
+        out_p = torch.from_numpy(np.ascontiguousarray(p).view(np.int64).reshape(-1))
+        counts = torch.from_numpy(c)
+    via_host = _host_collectives(out_h)
     send_counts = counts.cpu() if via_host else counts
     recv_counts = torch.empty_like(send_counts)
     dist.all_to_all_single(recv_counts, send_counts)
-    in_splits = [2 * int(c) for c in send_counts.tolist()]
-    out_splits = [2 * int(c) for c in recv_counts.tolist()]
-    src = out.cpu() if via_host else out
-    recv = torch.empty(sum(out_splits), dtype=torch.int64, device=src.device)
-    dist.all_to_all_single(recv, src, out_splits, in_splits)
-    return recv.to(hashes.device) if via_host else recv
+    sc, rc = send_counts.tolist(), recv_counts.tolist()   # the exchange's one host synchronisation
+    src_h = out_h.cpu() if via_host else out_h
+    src_p = out_p.cpu() if via_host else out_p
+    recv_h = torch.empty(2 * sum(rc), dtype=torch.int64, device=src_h.device)
+    recv_p = torch.empty(W * sum(rc), dtype=torch.int64, device=src_p.device)
+    dist.all_to_all_single(recv_h, src_h, [2 * c for c in rc], [2 * c for c in sc])
+    dist.all_to_all_single(recv_p, src_p, [W * c for c in rc], [W * c for c in sc])
+    if via_host:
+        return recv_h.to(hashes.device), recv_p.to(hashes.device)
+    return recv_h, recv_p
 
 
 def _all_reduce_pairs(pairs, pair_bound, stream):
@@ -168,49 +190,70 @@ def _all_reduce_pairs(pairs, pair_bound, stream):
         dist.all_reduce(pairs, op=dist.ReduceOp.SUM)
 
 
-def combine(counts, pairs, hashes, table=None, stream=None, pair_bound=None):
+def _all_reduce(t):
+    import torch.distributed as dist
+    if _host_collectives(t):
+        h = t.cpu()
+        dist.all_reduce(h, op=dist.ReduceOp.SUM)
+        t.copy_(h)
+    else:
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+
+
+def combine(counts, pairs, hashes, panels, W, table=None, stream=None, pair_bound=None, status=None):
     """Exchange steps for this rank; returns (counts, pairs, unique_tensor).
 
-    counts int64[n], pairs int64[n*n] or None, hashes int64[2*S_local] (this rank's
-    panel hashes).  Counts and pairs: all_reduce(SUM).  Distinct panels: every hash goes to
-    its owner rank (exchange_hashes, one all_to_all), the owner counts its distinct hashes
-    (device hash table on GPU tensors, numpy on CPU), all_reduce(SUM) of the counts.
+    counts int64[n], pairs int64[n*n] or None, hashes int64[2*S_local] and panels
+    int64[S_local*W] (this rank's panels).  Counts and pairs: all_reduce(SUM).  Distinct
+    panels: every panel goes to its owner rank (exchange_panels), the owner counts its distinct
+    panels exactly (device: csa_unique_async with bitmask comparison, table overflow reported in
+    ``status``; host: numpy), all_reduce(SUM) of the counts.
     """
     import torch
-    import torch.distributed as dist
-    if _host_collectives(counts):
-        h = counts.cpu()
-        dist.all_reduce(h, op=dist.ReduceOp.SUM)
-        counts.copy_(h)
-    else:
-        dist.all_reduce(counts, op=dist.ReduceOp.SUM)
+    _all_reduce(counts)
     if pairs is not None:
         _all_reduce_pairs(pairs, pair_bound, stream)
-    mine = exchange_hashes(hashes, stream)
-    if mine.is_cuda:
+    mine_h, mine_p = exchange_panels(hashes, panels, W, stream)
+    m = mine_h.numel() // 2
+    if mine_h.is_cuda:
         from . import _native as N
         if table is None:
-            table = HashTable(mine.numel() // 2, mine.device)
-        table.ensure(mine.numel() // 2)
+            table = HashTable(m, mine_h.device)
+        table.ensure(m)
         table.count.zero_()
-        sp = ctypes.c_void_p((stream or torch.cuda.current_stream(mine.device)).cuda_stream)
-        N.check(N.lib().csa_unique_hashes_async(N.ptr(mine), mine.numel() // 2, 1, 0, N.ptr(table.table),
-                                                table.slots, N.ptr(table.count), sp))
+        sp = ctypes.c_void_p((stream or torch.cuda.current_stream(mine_h.device)).cuda_stream)
+        N.check(N.lib().csa_unique_async(N.ptr(mine_h), N.ptr(mine_p), m, W, N.ptr(table.table), table.slots,
+                                         N.ptr(table.count), N.ptr(status), sp))
         u = table.count.clone()
     else:
-        m = mine.numpy().view(np.uint64).reshape(-1, 2)
-        u = torch.tensor([int(len(np.unique(m, axis=0))) if len(m) else 0], dtype=torch.int64)
-    if _host_collectives(u):
-        h = u.cpu()
-        dist.all_reduce(h, op=dist.ReduceOp.SUM)
-        u.copy_(h)
-    else:
-        dist.all_reduce(u, op=dist.ReduceOp.SUM)
+        u = torch.tensor([distinct_exact(mine_h.numpy().view(np.uint64), mine_p.numpy().view(np.uint64).reshape(m, W))],
+                         dtype=torch.int64)
+    _all_reduce(u)
     return counts, pairs, u
 
 
-def legacy_probabilities_distributed(instance, iterations, random_seed, keep_panels=False):
-    """analysis.py:162-191 with the panels sharded over the ranks of the default group."""
+def gather_panels(panels, S, W):
+    """All ranks' shards (contiguous global ranges, shard_range) -> uint64[S, W] on every rank."""
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size()
+    per = shard_range(S, world, 0)[1]
+    buf = torch.zeros(per * W, dtype=torch.int64, device=panels.device)
+    buf[: panels.numel()] = panels
+    src = buf.cpu() if _host_collectives(buf) else buf
+    parts = [torch.empty_like(src) for _ in range(world)]
+    dist.all_gather(parts, src)
+    rows = []
+    for r, t in enumerate(parts):
+        b, e = shard_range(S, world, r)
+        rows.append(t.cpu().numpy().view(np.uint64).reshape(per, W)[: e - b])
+    return np.concatenate(rows) if rows else np.zeros((0, W), np.uint64)
+
+
+def legacy_probabilities_distributed(instance, iterations, random_seed, keep_panels=True):
+    """analysis.py:162-191 with the panels sharded over the ranks of the default group.  Every rank
+    returns the whole job's results; with ``keep_panels`` every rank gathers all panels so that
+    ``found_panels`` iterates like the reference's set (costs S*W*8 bytes per rank)."""
     import torch
     from . import analysis as A
     from .device import DevicePipeline
@@ -223,12 +266,18 @@ def legacy_probabilities_distributed(instance, iterations, random_seed, keep_pan
     enc.check_quotas(instance.k)
     begin, end = shard_range(S, world, r)
     local = end - begin
-    torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", r)))
+    # one process per GPU (LOCAL_RANK); the modulo lets rehearsals put several ranks on one device
+    torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", r)) % max(torch.cuda.device_count(), 1))
     pipe = DevicePipeline(enc, instance.k, max(local, 1), want_pairs=True, want_unique=True)
     pipe.reset()
     if local:
-        pipe.run(random_seed, begin, local)
+        pipe.draw(random_seed, begin, local)
+        pipe.transpose_count(local)
+        pipe.pair_counts(local)
     pipe.check_status()
-    counts, pairs, u = combine(pipe.counts, pipe.pairs, pipe.hashes[: 2 * local], pair_bound=S)
-    raw = A.LegacyRaw(counts.cpu().numpy(), pairs.cpu().numpy().reshape(enc.n, enc.n), int(u.item()), None, None)
+    counts, pairs, u = combine(pipe.counts, pipe.pairs, pipe.hashes[: 2 * local], pipe.panels[: local * enc.W],
+                               enc.W, pair_bound=S, status=pipe.status)
+    pipe.check_status()
+    panels = gather_panels(pipe.panels[: local * enc.W], S, enc.W) if keep_panels else None
+    raw = A.LegacyRaw(counts.cpu().numpy(), pairs.cpu().numpy().reshape(enc.n, enc.n), int(u.item()), panels, None)
     return A.finish(instance, enc, raw, S)

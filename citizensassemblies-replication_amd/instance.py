@@ -95,6 +95,10 @@ class EncodedInstance:
             N.check(L.csa_instance_create(self.n, self.C, self.F, N.ptr(self.person_feat), N.ptr(self.fmin),
                                           N.ptr(self.fmax), N.ptr(self.fcat), ctypes.byref(h)))
             self._handle = h
+            # the dicts' own "selected" / "remaining" counters are the draw's start state, as in
+            # the reference's deep copies (analysis.py:147-148); the device default is 0 / pool
+            if np.any(self.sel0 != 0) or not np.array_equal(self.rem0, self.pool):
+                N.check(L.csa_instance_set_state(h, N.ptr(self.sel0), N.ptr(self.rem0), None))
         return self._handle
 
     def close(self):

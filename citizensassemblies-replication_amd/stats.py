@@ -78,6 +78,11 @@ def sorted_pair_probabilities(pair_histogram, device="cuda"):
         return np.sort(pair_histogram.upper())      # float histogram: not a LEGACY count matrix
     import torch
     n = counts.shape[0]
-    n_bins = int(np.max(np.diagonal(counts))) + 1 if n else 1   # pair count <= both person counts
-    d = torch.from_numpy(np.ascontiguousarray(counts, np.int64)).to(device)
-    return sorted_counts_to_probabilities(pair_count_histogram(d, n, n_bins), S)
+    if isinstance(counts, np.ndarray):
+        d = torch.from_numpy(np.ascontiguousarray(counts, np.int64)).to(device)
+    else:
+        d = counts.reshape(n, n)              # device counts kept by legacy_probabilities: no host copy
+    # every pair count is <= both person counts (the diagonal); the max over the triangle covers
+    # matrices whose diagonal was not kept as well
+    n_bins = int(torch.triu(d).max().item()) + 1 if n else 1
+    return sorted_counts_to_probabilities(pair_count_histogram(d.contiguous().view(-1), n, n_bins), S)

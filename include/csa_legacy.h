@@ -134,6 +134,20 @@ int csa_draw_async(const csa_instance *inst, int32_t k, uint64_t seed, uint64_t 
                    uint64_t *d_hashes, uint32_t *d_attempts, int32_t *d_picks,
                    uint32_t *d_status, void *stream);
 
+/* The same draw split in two, for instances whose batch draw is the pick-list kernel
+ * (draw_lane_kernel: F <= 32, n <= 2048; csa_draw_picks_supported returns 1 for them, else 0 and
+ * csa_draw_picks_async returns CSA_E_UNSUPPORTED).  csa_draw_picks_async writes each panel's k
+ * picks in pick order (d_picks: n_panels*k uint16; legacy.py:194 people_selected order);
+ * csa_picks_pack_async turns pick lists into packed panels (n_panels*W) and, if d_hashes is not
+ * NULL, their 128-bit hashes.  csa_draw_async = the two back to back on one stream (with an
+ * instance-owned pick buffer: concurrent csa_draw_async calls on one instance serialise). */
+int csa_draw_picks_supported(const csa_instance *inst, int32_t k);
+int csa_draw_picks_async(const csa_instance *inst, int32_t k, uint64_t seed, uint64_t panel_begin,
+                         uint64_t n_panels, uint32_t max_attempts, uint16_t *d_picks, uint32_t *d_attempts,
+                         uint32_t *d_status, void *stream);
+int csa_picks_pack_async(const uint16_t *d_picks, uint64_t n_panels, int32_t k, int32_t n, uint64_t *d_panels,
+                         uint64_t *d_hashes, void *stream);
+
 /* 128-bit panel hashes (2*n_panels uint64) of packed panels (n_panels*W), the
  * key of the distinct-panel count (replaces hashing the sorted tuples of
  * analysis.py:171,186); identical to the hashes csa_draw_async writes. */
@@ -141,7 +155,7 @@ int csa_panel_hash_async(const uint64_t *d_panels, uint64_t n_panels, int32_t W,
                          void *stream);
 
 /* Name of the draw kernel csa_draw_async launches for this instance and k
- * (e.g. "draw_batch_kernel<4, 8, 8>"), for matching profiler output. */
+ * (e.g. "draw_lane_kernel<32, 28, 14>"), for matching profiler output. */
 int csa_draw_kernel_name(const csa_instance *inst, int32_t k, char *buf, uint64_t len);
 
 /* Bit-transpose + per-person count.  Panels (n_panels*W) -> d_xt, the
@@ -179,20 +193,15 @@ int csa_pair_counts_ex_async(const uint64_t *d_xt, uint64_t n_blocks, int32_t n,
 int csa_pair_counts_async(const uint64_t *d_xt, uint64_t n_blocks, int32_t n, int64_t *d_pairs,
                           void *stream);
 
-/* Distinct-panel count: open-addressing table of panel indices keyed by the
- * 128-bit hashes, with full-bitmask comparison when d_panels != NULL (exact).
- * d_table: table_slots uint64 (power of two >= 2*n_panels), zeroed by the
- * call; *d_unique (uint64) is ACCUMULATED. */
-int csa_unique_async(const uint64_t *d_hashes, const uint64_t *d_panels, uint64_t n_panels,
-                     int32_t W, uint64_t *d_table, uint64_t table_slots, uint64_t *d_unique,
+/* Distinct-panel count (found_panels, analysis.py:171,186): two panels are the same iff their
+ * 128-bit hashes AND their W-word bitmasks are equal, so the count is exact.  d_panels (n_panels*W)
+ * is required.  d_table: table_slots uint64 (power of two >= 2*n_panels) of scratch; *d_unique
+ * (uint64) is ACCUMULATED.  With d_status (the 4-word status block) batches of >= 65536 panels take a
+ * partitioned path (per-partition LDS tables, no per-panel global atomics); a partition table that
+ * overflows sets CSA_E_UNSUPPORTED there.  With d_status == NULL the single global table runs. */
+int csa_unique_async(const uint64_t *d_hashes, const uint64_t *d_panels, uint64_t n_panels, int32_t W,
+                     uint64_t *d_table, uint64_t table_slots, uint64_t *d_unique, uint32_t *d_status,
                      void *stream);
-
-/* Multi-GPU distinct-panel step: insert the 128-bit hashes (2*n_hashes
- * uint64, e.g. every rank's hashes after an all-gather) whose owner
- * h1 % world equals `rank`, comparing hashes only; *d_unique is ACCUMULATED.
- * Summing the per-rank results (all-reduce) gives the global count. */
-int csa_unique_hashes_async(const uint64_t *d_hashes, uint64_t n_hashes, uint32_t world, uint32_t rank,
-                            uint64_t *d_table, uint64_t table_slots, uint64_t *d_unique, void *stream);
 
 /* Histogram of the pair counts d_pairs[i][j], i < j (n*n int64, row-major, as
  * produced by csa_pair_counts_*): d_hist[v] (n_bins uint64, zeroed by the call)
@@ -204,14 +213,16 @@ int csa_unique_hashes_async(const uint64_t *d_hashes, uint64_t n_hashes, uint32_
 int csa_pair_histogram_async(const int64_t *d_pairs, int32_t n, uint64_t *d_hist, uint64_t n_bins,
                              uint64_t *d_overflow, void *stream);
 
-/* Multi-GPU distinct-panel exchange, send side: bucket the 128-bit hashes
- * (2*n_hashes uint64) by owner rank h1 % world into d_out (2*n_hashes uint64,
- * owner-major, any order inside a bucket); d_counts (world uint64) = hashes
- * per owner, d_cursor (world uint64) scratch.  The buckets feed an
- * all_to_all; each rank then counts its received hashes with
- * csa_unique_hashes_async(world = 1, rank = 0).  world <= 1024. */
-int csa_hash_buckets_async(const uint64_t *d_hashes, uint64_t n_hashes, uint32_t world, uint64_t *d_out,
-                           uint64_t *d_counts, uint64_t *d_cursor, void *stream);
+/* Multi-GPU distinct-panel exchange, send side: bucket the 128-bit hashes (2*n_hashes uint64)
+ * by owner rank h1 % world into d_out (2*n_hashes uint64, owner-major, any order inside a
+ * bucket) and, with d_panels (n_hashes*W), the panels' bitmasks alongside into d_out_panels
+ * (n_hashes*W, same order); d_counts (world uint64) = panels per owner, d_cursor (world uint64)
+ * scratch.  The buckets feed an all_to_all; each owner then counts its distinct panels exactly
+ * with csa_unique_async (equal panels have equal hashes, so they meet at one owner).
+ * world <= 1024. */
+int csa_hash_buckets_async(const uint64_t *d_hashes, const uint64_t *d_panels, uint64_t n_hashes, int32_t W,
+                           uint32_t world, uint64_t *d_out, uint64_t *d_out_panels, uint64_t *d_counts,
+                           uint64_t *d_cursor, void *stream);
 
 /* Multi-GPU pair exchange: pack the upper triangle incl. the diagonal of the
  * n*n int64 pair counts row-major into n(n+1)/2 int32 (every count must be

@@ -1,9 +1,14 @@
-"""World-size-2 gloo rehearsal of the multi-GPU exchange (distributed.combine) on CPU.
+"""World-size-2/3 gloo rehearsal of the multi-GPU exchange (distributed.combine) on CPU.
 
 Each rank produces its contiguous shard of panels with the C oracle (standing in
-for that rank's GPU), then runs the real exchange code: all_reduce of counts and
-pair counts, all_gather of 128-bit panel hashes + owner-partition dedupe +
-all_reduce.  The combined results must equal one unsharded run.
+for that rank's GPU), then runs the real exchange code on host tensors: all_reduce
+of counts and pair counts, all_to_all of every panel (128-bit hash + bitmask) to
+its owner rank h1 % world through the host mirror of csa_hash_buckets_async, the
+owner's exact dedupe (host mirror of csa_unique_async: equal hash AND equal
+bitmask), all_reduce of the owners' counts.  The combined results must equal one
+unsharded run -- on an all-distinct instance and on a duplicate-heavy one whose
+duplicates land on different ranks -- and two different panels given the same
+128-bit hash must still count twice (the count is exact, not hash-based).
 """
 import os
 import socket
@@ -16,7 +21,7 @@ import torch.multiprocessing as mp
 
 from conftest import REPO, inst_paths, pkg
 
-S, SEED, NAME, K = 3000, 5, "sf_e_110", 110
+CASES = {"sf_e_110": (110, 3000, 5), "couples_panel_from_twenty_people_no_constraints_2": (2, 3000, 7)}
 
 
 def _free_port():
@@ -25,24 +30,31 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, out_dir):
+def _init(rank, world, port):
     import sys
     sys.path.insert(0, REPO)
     sys.path.insert(0, os.path.join(REPO, "tests"))
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
+
+
+def _worker(rank, world, port, out_dir, name):
+    _init(rank, world, port)
     from oracle import coracle
     from oracle.legacy_oracle import read_instance
     D = pkg("distributed")
-    o = read_instance(*inst_paths(NAME), K)
+    K, S, SEED = CASES[name]
+    o = read_instance(*inst_paths(name), K)
     b, e = D.shard_range(S, world, rank)
     rc, panels, _, _ = coracle.draw(o, K, SEED, b, e - b, threads=2)
     assert rc == 0
+    W = panels.shape[1]
     counts = torch.from_numpy(coracle.counts(panels, o.n))
     pairs = torch.from_numpy(coracle.pairs(panels, o.n, threads=2).ravel().copy())
     hashes = torch.from_numpy(D.panel_hashes(panels).ravel().view(np.int64).copy())
-    counts, pairs, u = D.combine(counts, pairs, hashes)
+    ptens = torch.from_numpy(np.ascontiguousarray(panels).view(np.int64).ravel().copy())
+    counts, pairs, u = D.combine(counts, pairs, hashes, ptens, W)
     if rank == 0:
         np.save(os.path.join(out_dir, "counts.npy"), counts.numpy())
         np.save(os.path.join(out_dir, "pairs.npy"), pairs.numpy())
@@ -51,18 +63,77 @@ def _worker(rank, world, port, out_dir):
     dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("name", sorted(CASES))
 @pytest.mark.parametrize("world", [2, 3])
-def test_gloo_exchange_matches_single_run(tmp_path, world):
+def test_gloo_exchange_matches_single_run(tmp_path, world, name):
     from oracle import coracle
     from oracle.legacy_oracle import read_instance
-    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
-    o = read_instance(*inst_paths(NAME), K)
+    K, S, SEED = CASES[name]
+    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path), name), nprocs=world, join=True)
+    o = read_instance(*inst_paths(name), K)
     rc, panels, _, _ = coracle.draw(o, K, SEED, 0, S, threads=4)
     assert rc == 0
     assert np.array_equal(np.load(tmp_path / "counts.npy"), coracle.counts(panels, o.n))
     full = coracle.pairs(panels, o.n, threads=4).ravel()
     assert np.array_equal(np.load(tmp_path / "pairs.npy"), full)
-    assert int(np.load(tmp_path / "unique.npy")[0]) == coracle.unique(panels, o.n)
+    want = coracle.unique(panels, o.n)
+    if name.startswith("couples"):
+        # duplicates really are split across ranks: every shard holds most of the 100 panels
+        assert want == 100
+    assert int(np.load(tmp_path / "unique.npy")[0]) == want
+
+
+def _collision_worker(rank, world, port, out_dir):
+    """Rank 0 holds panel A; rank 1 holds a different panel B and another copy of A, all three
+    under the SAME (fake) 128-bit hash: the exact count is 2, a hash-only count would be 1."""
+    _init(rank, world, port)
+    D = pkg("distributed")
+    W = 3
+    A = np.array([1, 2, 3], np.uint64)
+    B = np.array([1, 2, 4], np.uint64)
+    rows = [A] if rank == 0 else [B, A]
+    panels = torch.from_numpy(np.stack(rows).view(np.int64).ravel().copy())
+    fake = np.tile(np.array([12345, 678], np.uint64), (len(rows), 1))
+    hashes = torch.from_numpy(fake.view(np.int64).ravel().copy())
+    counts = torch.zeros(4, dtype=torch.int64)
+    _, _, u = D.combine(counts, None, hashes, panels, W)
+    if rank == 0:
+        np.save(os.path.join(out_dir, "unique.npy"), np.array([int(u.item())]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gloo_exchange_exact_on_hash_collision(tmp_path):
+    mp.spawn(_collision_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+    assert int(np.load(tmp_path / "unique.npy")[0]) == 2
+
+
+def test_owner_buckets_mirror():
+    """owner_buckets (host mirror of csa_hash_buckets_async): owner-major, every panel travels with
+    its hash, per-owner counts."""
+    D = pkg("distributed")
+    rng = np.random.default_rng(3)
+    p = rng.integers(0, 2 ** 63, size=(1000, 5), dtype=np.int64).astype(np.uint64)
+    h = D.panel_hashes(p)
+    for world in (1, 2, 3, 8):
+        bh, bp, c = D.owner_buckets(h, p, world)
+        assert c.sum() == 1000 and len(c) == world
+        assert np.array_equal(D.panel_hashes(bp), bh)
+        start = 0
+        for w in range(world):
+            assert np.all(bh[start:start + c[w], 0] % np.uint64(world) == np.uint64(w))
+            start += c[w]
+        assert sorted(map(tuple, bp.tolist())) == sorted(map(tuple, p.tolist()))
+
+
+def test_distinct_exact_mirror():
+    D = pkg("distributed")
+    p = np.array([[1, 2], [1, 2], [1, 3], [0, 0]], np.uint64)
+    h = D.panel_hashes(p)
+    assert D.distinct_exact(h, p) == 3
+    h[2] = h[0]          # a forged collision still counts as a different panel
+    assert D.distinct_exact(h, p) == 3
+    assert D.distinct_exact(np.zeros((0, 2), np.uint64), np.zeros((0, 2), np.uint64)) == 0
 
 
 def test_panel_hash_mirror_is_sensitive():

@@ -1,9 +1,10 @@
 """GPU parity of every draw-kernel layout against the C oracle (Philox verification mode).
 
-The batch path picks draw_batch_kernel (G = 4 / 8 lanes per panel) or draw_kernel
-(G = 16 / 64) from the instance shape; CSA_DRAW_GROUP forces a layout.  Each must
-give the oracle's panels and attempt counts bit-exactly, including the edge cases
-of legacy.py:124-200 (restarts, rejections, max = 0 features, max = 0 < min).
+The batch path picks draw_lane_kernel (2 lanes per panel, pick lists packed by
+picks_pack_kernel) or draw_kernel (G = 16 / 64) from the instance shape;
+CSA_DRAW_KERNEL=lane|16|64 forces a layout the instance fits.  Each must give the
+oracle's panels and attempt counts bit-exactly, including the edge cases of
+legacy.py:124-200 (restarts, rejections, max = 0 features, max = 0 < min).
 """
 import os
 
@@ -19,25 +20,16 @@ pytestmark = pytest.mark.gpu
 
 @pytest.fixture
 def draw_group():
-    """Force a draw layout: an int G selects CSA_DRAW_GROUP=G (batch / general kernels, 1 = lane
-    kernel with one lane per panel); "2L" / "4L" select the lane kernel with 2 / 4 lanes per panel
-    (CSA_DRAW_LANE)."""
-    names = ("CSA_DRAW_GROUP", "CSA_DRAW_LANE")
-    old = {k: os.environ.get(k) for k in names}
+    """Force a batch draw layout (CSA_DRAW_KERNEL = "lane" / "16" / "64")."""
+    old = os.environ.get("CSA_DRAW_KERNEL")
 
     def set_layout(g):
-        for k in names:
-            os.environ.pop(k, None)
-        if isinstance(g, str) and g.endswith("L"):
-            os.environ["CSA_DRAW_LANE"] = g[:-1]
-        else:
-            os.environ["CSA_DRAW_GROUP"] = str(g)
+        os.environ["CSA_DRAW_KERNEL"] = str(g)
     yield set_layout
-    for k, v in old.items():
-        if v is None:
-            os.environ.pop(k, None)
-        else:
-            os.environ[k] = v
+    if old is None:
+        os.environ.pop("CSA_DRAW_KERNEL", None)
+    else:
+        os.environ["CSA_DRAW_KERNEL"] = old
 
 
 def _sample(enc, k, S, seed, begin=0, max_attempts=0):
@@ -49,7 +41,7 @@ def _sample(enc, k, S, seed, begin=0, max_attempts=0):
     return panels, attempts
 
 
-@pytest.mark.parametrize("group", [1, "2L", "4L", 4, 8, 16, 64])
+@pytest.mark.parametrize("group", ["lane", 16, 64])
 @pytest.mark.parametrize("name,k,S,seed", [("sf_e_tight_110", 110, 3000, 5), ("pathological_5", 5, 4000, 2),
                                            ("rejecty_6", 6, 20000, 8), ("example_small_20", 20, 20000, 1),
                                            ("couples_panel_from_twenty_people_no_constraints_2", 2, 20000, 3)])
@@ -77,7 +69,7 @@ def _weird_instance():
     return cats, agents
 
 
-@pytest.mark.parametrize("group", [1, "2L", "4L", 4, 8, 16, 64])
+@pytest.mark.parametrize("group", ["lane", 16, 64])
 def test_zero_max_features_match_oracle(gpu_available, draw_group, group):
     """max = 0 features (dead, and max = 0 < min which routes to draw_kernel) vs the oracle."""
     P = pkg()
@@ -97,3 +89,76 @@ def test_zero_max_features_match_oracle(gpu_available, draw_group, group):
     assert rc == 0
     assert np.array_equal(attempts, oatt)
     assert np.array_equal(panels, opanels)
+
+
+@pytest.mark.parametrize("name,k,S,seed", [("sf_e_tight_110", 110, 3000, 5), ("example_small_20", 20, 5000, 3),
+                                           ("pathological_5", 5, 4000, 2)])
+def test_pick_lists_match_oracle_pick_order(gpu_available, name, k, S, seed):
+    """csa_draw_picks_async writes each accepted panel's picks in pick order (the order of
+    people_selected, legacy.py:194); csa_picks_pack_async packs them (+ hashes) bit-exactly."""
+    import torch
+    P = pkg()
+    N = pkg("_native")
+    D = pkg("distributed")
+    inst = P.read_instance(*inst_paths(name), k)
+    enc = P.encode(inst.categories, inst.agents)
+    assert N.lib().csa_draw_picks_supported(enc.handle, k) == 1
+    begin = 4242
+    picks = torch.empty(S * k, dtype=torch.int16, device="cuda")
+    att = torch.empty(S, dtype=torch.int32, device="cuda")
+    status = torch.zeros(4, dtype=torch.int32, device="cuda")
+    N.check(N.lib().csa_draw_picks_async(enc.handle, k, seed, begin, S, 0, N.ptr(picks), N.ptr(att), N.ptr(status),
+                                         None))
+    panels = torch.empty(S * enc.W, dtype=torch.int64, device="cuda")
+    hashes = torch.empty(2 * S, dtype=torch.int64, device="cuda")
+    N.check(N.lib().csa_picks_pack_async(N.ptr(picks), S, k, enc.n, N.ptr(panels), N.ptr(hashes), None))
+    torch.cuda.synchronize()
+    assert int(status[0].item()) == 0
+    o = oracle_read(*inst_paths(name), k)
+    rc, opanels, oatt, opicks = coracle.draw(o, k, seed, begin, S, want_picks=True)
+    assert rc == 0
+    assert np.array_equal(picks.cpu().numpy().astype(np.int32).reshape(S, k), opicks)
+    assert np.array_equal(att.cpu().numpy().astype(np.uint32), oatt)
+    got = panels.cpu().numpy().view(np.uint64).reshape(S, enc.W)
+    assert np.array_equal(got, opanels)
+    assert np.array_equal(hashes.cpu().numpy().view(np.uint64).reshape(S, 2), D.panel_hashes(opanels))
+
+
+@pytest.mark.parametrize("S", [1, 63, 64, 65, 1000, 4097])
+def test_picks_pack_edges(gpu_available, S):
+    """picks_pack_kernel on ragged batch tails and odd k (u32 loads of two picks, a single last
+    pick), checked against a host packing of random distinct picks."""
+    import torch
+    N = pkg("_native")
+    D = pkg("distributed")
+    rng = np.random.default_rng(S)
+    for n, k in ((200, 7), (1727, 110), (64, 1), (2048, 33)):
+        picks = np.stack([rng.choice(n, size=k, replace=False) for _ in range(S)]).astype(np.int16)
+        want = np.zeros((S, (n + 63) // 64), np.uint64)
+        for i in range(S):
+            for p in picks[i].astype(np.int64):
+                want[i, p >> 6] |= np.uint64(1) << np.uint64(p & 63)
+        d = torch.from_numpy(picks.ravel().copy()).cuda()
+        W = (n + 63) // 64
+        panels = torch.full((S * W,), -1, dtype=torch.int64, device="cuda")
+        hashes = torch.empty(2 * S, dtype=torch.int64, device="cuda")
+        N.check(N.lib().csa_picks_pack_async(N.ptr(d), S, k, n, N.ptr(panels), N.ptr(hashes), None))
+        torch.cuda.synchronize()
+        assert np.array_equal(panels.cpu().numpy().view(np.uint64).reshape(S, W), want)
+        assert np.array_equal(hashes.cpu().numpy().view(np.uint64).reshape(S, 2), D.panel_hashes(want))
+
+
+def test_k_zero_draws_empty_panels(gpu_available):
+    """k = 0 (legacy.py:184 loops zero times): empty panels accepted at the first attempt when no
+    feature has min > 0, else the reference restarts forever -> attempt limit."""
+    P = pkg()
+    N = pkg("_native")
+    cats = {"a": {"x": {"min": 0, "max": 2}, "y": {"min": 0, "max": 2}}}
+    agents = {i: {"a": "x" if i % 2 else "y"} for i in range(10)}
+    enc = P.encode(cats, agents)
+    panels, attempts = _sample(enc, 0, 100, 3)
+    assert not panels.any() and np.all(attempts == 1)
+    cats["a"]["x"]["min"] = 1
+    enc = P.encode(cats, agents)
+    with pytest.raises(N.CsaError):
+        _sample(enc, 0, 10, 3, max_attempts=5)

@@ -106,3 +106,34 @@ def test_pair_fp4_exact_beyond_f32_range(gpu_available):
     assert int(P[n - 1, n - 1]) == S
     assert int(P[0, 1]) == c1 and int(P[1, 1]) == c1 and int(P[1, n - 1]) == c1
     assert int(P[2, 3]) == 0 and int(P[0, 2]) == 0
+
+
+@pytest.mark.parametrize("engine", [0, 1])
+def test_pairs_n8192_vs_torch_fp32(gpu_available, engine):
+    """BASELINE config 5 shape: n = 8192 (32 triangle rows of 256 x 256 blocks), S = 131072 panels of
+    ~2.5 % density (k ~ 200), against a plain PyTorch fp32 X^T X on the device (rocBLAS; exact:
+    every partial sum <= S < 2^24, and gfx950 has no reduced-precision fp32 GEMM mode)."""
+    import torch
+    N = pkg("_native")
+    n, S = 8192, 131072
+    npad = int(N.lib().csa_xt_pad(n))
+    nblk = S // 64
+    g = torch.Generator(device="cuda").manual_seed(8192 + engine)
+    X = (torch.rand(S, n, device="cuda", generator=g) < 0.025)
+    X[:, 17] = True                                              # a dense agent: counts up to S
+    # pack the transposed bits: xt[b, p] bit j = X[64 b + j, p]
+    w = (1 << torch.arange(64, device="cuda", dtype=torch.int64))
+    xt = torch.zeros(nblk, npad, dtype=torch.int64, device="cuda")
+    xt[:, :n] = (X.view(nblk, 64, n).to(torch.int64) * w.view(1, 64, 1)).sum(dim=1)
+    L = N.lib()
+    pairs = torch.full((n * n,), -7, dtype=torch.int64, device="cuda")
+    sb = int(L.csa_pair_scratch_bytes(n, nblk, engine))
+    scr = torch.empty((sb + 3) // 4, dtype=torch.int32, device="cuda")
+    N.check(L.csa_pair_counts_ex_async(N.ptr(xt), nblk, n, N.ptr(pairs), engine | N.CSA_PAIR_OVERWRITE, N.ptr(scr),
+                                       sb, None))
+    Xf = X.to(torch.float32)
+    ref = (Xf.T @ Xf).to(torch.int64)
+    torch.cuda.synchronize()
+    got = pairs.view(n, n)
+    assert torch.equal(torch.triu(got), torch.triu(ref))
+    assert int(ref[17, 17].item()) == S

@@ -91,7 +91,7 @@ def test_legacy_probabilities_api(gpu_available):
 
 @pytest.mark.parametrize("name,k,S,seed", [("sf_e_110", 110, 20000, 7), ("sf_e_tight_110", 110, 5000, 3),
                                            ("example_large_200", 200, 4000, 11),
-                                           ("synthetic8192_200", 200, 600, 5), ("rejecty_6", 6, 50000, 9)])
+                                           ("synthetic8192_200", 200, 100000, 5), ("rejecty_6", 6, 50000, 9)])
 def test_sample_matches_c_oracle(gpu_available, name, k, S, seed):
     A = pkg("analysis")
     inst, enc = _enc(name, k)
@@ -112,10 +112,8 @@ def test_sample_matches_c_oracle(gpu_available, name, k, S, seed):
     assert np.array_equal(attempts, oatt)
     assert np.array_equal(counts, coracle.counts(opanels, enc.n))
     assert int(uniq[0]) == coracle.unique(opanels, enc.n)
-    if enc.n <= 2000:
-        op = coracle.pairs(opanels, enc.n)
-        iu = np.triu_indices(enc.n, 1)
-        assert np.array_equal(pairs[iu], op[iu])
+    op = coracle.pairs(opanels, enc.n)          # n = 8192: 32 x 32 blocks of the 256 x 256 tiling
+    assert np.array_equal(np.triu(pairs), np.triu(op))
     assert np.array_equal(np.diag(pairs), counts)
 
 
@@ -234,26 +232,47 @@ def test_device_pipeline_matches_host_api(gpu_available):
     torch.cuda.synchronize()
 
 
-def test_unique_hashes_owner_partition(gpu_available):
-    """csa_unique_hashes_async (multi-GPU distinct-panel step): per-owner counts sum to the total."""
+def test_owner_partition_exact_on_device(gpu_available):
+    """Multi-GPU distinct-panel step on one device: csa_hash_buckets_async buckets panels (hash +
+    bitmask) by owner, csa_unique_async counts each owner's bucket exactly; the per-owner counts
+    sum to the global count for any world, and a forged hash collision between two different
+    panels still counts twice (bitmask comparison, not hash equality)."""
     import torch
     D = pkg("distributed")
     N = pkg("_native")
     o = oracle_read(*inst_paths("example_small_20"), 20)
     rc, panels, _, _ = coracle.draw(o, 20, 3, 0, 5000)
     panels = np.concatenate([panels, panels[:700]])           # 700 duplicates
-    h = torch.from_numpy(D.panel_hashes(panels).ravel().view(np.int64).copy()).cuda()
-    table = D.HashTable(h.numel() // 2, h.device)
-    total = 0
+    W = panels.shape[1]
+    hashes = D.panel_hashes(panels)
+    hashes[1000] = hashes[0]              # forged collision: panel 1000 (no duplicate) differs from panel 0
+    assert not np.array_equal(panels[0], panels[1000])
+    want = coracle.unique(panels, o.n)
+    assert want == 5000
+    h = torch.from_numpy(hashes.ravel().view(np.int64).copy()).cuda()
+    p = torch.from_numpy(panels.ravel().view(np.int64).copy()).cuda()
+    m = len(panels)
+    status = torch.zeros(4, dtype=torch.int32, device="cuda")
     for world in (1, 2, 3, 8):
+        out_h, out_p = torch.empty_like(h), torch.empty_like(p)
+        counts = torch.empty(world, dtype=torch.int64, device="cuda")
+        cursor = torch.empty(world, dtype=torch.int64, device="cuda")
+        N.check(N.lib().csa_hash_buckets_async(N.ptr(h), N.ptr(p), m, W, world, N.ptr(out_h), N.ptr(out_p),
+                                               N.ptr(counts), N.ptr(cursor), None))
+        torch.cuda.synchronize()
+        c = counts.cpu().numpy()
+        starts = np.concatenate([[0], np.cumsum(c)])
+        table = D.HashTable(m, h.device)
         total = 0
         for r in range(world):
+            a, b = int(starts[r]), int(starts[r + 1])
             table.count.zero_()
-            N.check(N.lib().csa_unique_hashes_async(N.ptr(h), h.numel() // 2, world, r, N.ptr(table.table),
-                                                    table.slots, N.ptr(table.count), None))
+            N.check(N.lib().csa_unique_async(N.ptr(out_h[2 * a:]), N.ptr(out_p[a * W:]), b - a, W, N.ptr(table.table),
+                                             table.slots, N.ptr(table.count), N.ptr(status), None))
             torch.cuda.synchronize()
             total += int(table.count.item())
-        assert total == coracle.unique(panels, o.n) == 5000
+        assert int(status[0].item()) == 0
+        assert total == want
 
 
 def test_device_hashes_match_host_mirror(gpu_available):
@@ -271,18 +290,27 @@ def test_device_hashes_match_host_mirror(gpu_available):
 
 @pytest.mark.parametrize("world", [1, 3, 8])
 def test_hash_buckets(gpu_available, world):
-    """csa_hash_buckets_async: owner-major buckets (h1 % world) holding exactly the input hashes."""
+    """csa_hash_buckets_async: owner-major buckets (h1 % world) holding exactly the input hashes,
+    each with its panel words alongside."""
     import torch
     N = pkg("_native")
     rng = np.random.default_rng(world)
+    W = 3
     h = rng.integers(0, 2 ** 63, size=(50001, 2), dtype=np.int64)
+    pn = np.concatenate([h, np.arange(50001, dtype=np.int64)[:, None]], axis=1)  # panel = (h1, h2, index)
     d = torch.from_numpy(h.reshape(-1)).cuda()
+    dp = torch.from_numpy(pn.reshape(-1).copy()).cuda()
     out = torch.empty_like(d)
+    outp = torch.empty_like(dp)
     counts = torch.empty(world, dtype=torch.int64, device="cuda")
     cursor = torch.empty(world, dtype=torch.int64, device="cuda")
-    N.check(N.lib().csa_hash_buckets_async(N.ptr(d), 50001, world, N.ptr(out), N.ptr(counts), N.ptr(cursor), None))
+    N.check(N.lib().csa_hash_buckets_async(N.ptr(d), N.ptr(dp), 50001, W, world, N.ptr(out), N.ptr(outp),
+                                           N.ptr(counts), N.ptr(cursor), None))
     torch.cuda.synchronize()
     o = out.cpu().numpy().reshape(-1, 2).view(np.uint64)
+    op = outp.cpu().numpy().reshape(-1, W)
+    assert np.array_equal(op[:, :2].view(np.uint64), o)              # every panel travelled with its hash
+    assert sorted(op[:, 2].tolist()) == list(range(50001))
     owner = h.view(np.uint64)[:, 0] % np.uint64(world)
     c = counts.cpu().numpy()
     assert c.tolist() == np.bincount(owner.astype(np.int64), minlength=world).tolist()
@@ -340,8 +368,8 @@ def test_combine_rccl_world1(gpu_available):
         port = sk.getsockname()[1]
     dist.init_process_group("nccl", init_method="tcp://127.0.0.1:%d" % port, rank=0, world_size=1)
     try:
-        counts, pairs, u = Dd.combine(pipe.counts, pipe.pairs, pipe.hashes[: 2 * S], stream=pipe.stream,
-                                      pair_bound=S)
+        counts, pairs, u = Dd.combine(pipe.counts, pipe.pairs, pipe.hashes[: 2 * S], pipe.panels[: S * enc.W], enc.W,
+                                      stream=pipe.stream, pair_bound=S, status=pipe.status)
         torch.cuda.synchronize()
         got_pairs = pairs.cpu().numpy().reshape(enc.n, enc.n)
     finally:
@@ -374,3 +402,47 @@ def test_unique_partitioned_matches_oracle(gpu_available, name, k, S):
         finally:
             os.environ.pop("CSA_UNIQUE_PART", None)
     assert got["1"] == got["0"] == want
+
+
+def _dist_worker(rank, world, port, out_dir, name, k, S, seed):
+    import os
+    import sys
+    import torch.distributed as dist
+    from conftest import REPO
+    sys.path.insert(0, REPO)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        A = pkg("analysis")
+        inst = pkg().read_instance(*inst_paths(name), k)
+        alloc, found, hist = A.legacy_probabilities(inst, S, seed)      # world > 1: sharded
+        if rank == world - 1:
+            np.save(os.path.join(out_dir, "alloc.npy"), np.array([alloc[i] for i in range(len(alloc))]))
+            np.save(os.path.join(out_dir, "upper.npy"), hist.upper())
+            np.save(os.path.join(out_dir, "unique.npy"), np.array([len(found)]))
+            np.save(os.path.join(out_dir, "found.npy"), np.array(sorted(found)))
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("name,k,S,seed", [("sf_e_110", 110, 9001, 3),
+                                           ("couples_panel_from_twenty_people_no_constraints_2", 2, 5000, 1)])
+def test_legacy_probabilities_distributed_gloo(gpu_available, tmp_path, name, k, S, seed):
+    """analysis.legacy_probabilities with a 2-rank process group (both ranks on this GPU, gloo:
+    RCCL refuses two ranks on one device): the sharded draw, the exact panel exchange and the
+    gathered found_panels equal the single-GPU result."""
+    import socket
+    import torch.multiprocessing as mp
+    A = pkg("analysis")
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    mp.spawn(_dist_worker, args=(2, port, str(tmp_path), name, k, S, seed), nprocs=2, join=True)
+    inst = pkg().read_instance(*inst_paths(name), k)
+    alloc, found, hist = A.legacy_probabilities(inst, S, seed)
+    assert np.load(tmp_path / "alloc.npy").tolist() == [alloc[i] for i in range(len(alloc))]
+    assert np.array_equal(np.load(tmp_path / "upper.npy"), hist.upper())
+    assert int(np.load(tmp_path / "unique.npy")[0]) == len(found)
+    assert np.load(tmp_path / "found.npy").tolist() == [list(p) for p in sorted(found)]

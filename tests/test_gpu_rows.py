@@ -26,6 +26,8 @@ def test_run_legacy_or_retrieve_golden(gpu_available, tmp_path):
         assert len(found) == g["unique"]
         assert tuple(g["first_panels"][0]) in found
         assert hist.upper().tolist() == (np.asarray(g["pair_upper"]) / g["S"]).tolist()
+        # the pair-curve consumer works on a retrieved result as on a fresh one
+        assert pkg("stats").sorted_pair_probabilities(hist).tolist() == sorted(hist.upper().tolist())
 
 
 def test_run_legacy_or_retrieve_resample_seed(gpu_available, tmp_path):

@@ -81,13 +81,19 @@ def test_shard_range_covers_exactly():
             assert prev == S
 
 
-def test_hash_partition_dedupe():
+def test_owner_partition_dedupe():
+    """Distinct panels summed over owner partitions (owner = h1 % world) == the global count, for
+    any world: equal panels have equal hashes, so they always meet at one owner."""
     D = pkg("distributed")
     rng = np.random.default_rng(0)
-    h = rng.integers(0, 2 ** 63, size=(500, 2), dtype=np.int64).astype(np.uint64)
-    h = np.concatenate([h, h[:100]])                       # 100 duplicates
-    total = sum(D.dedupe_hash_partition(h.ravel(), 4, r) for r in range(4))
-    assert total == 500
+    p = rng.integers(0, 2 ** 63, size=(500, 4), dtype=np.int64).astype(np.uint64)
+    p = np.concatenate([p, p[:100]])                       # 100 duplicates
+    h = D.panel_hashes(p)
+    for world in (1, 2, 4, 7):
+        bh, bp, c = D.owner_buckets(h, p, world)
+        starts = np.concatenate([[0], np.cumsum(c)])
+        total = sum(D.distinct_exact(bh[starts[r]:starts[r + 1]], bp[starts[r]:starts[r + 1]]) for r in range(world))
+        assert total == 500
 
 
 def test_legacy_stream_positions():

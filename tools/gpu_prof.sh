@@ -11,7 +11,7 @@ OUT=$ROOT/gpurun_out/prof_$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 cd /tmp
-BENCH=("$ROOT/bench.py" --steps 3 --warmup 1 --no-cpu-baseline "$@")
+BENCH=("$ROOT/bench.py" --steps 3 --warmup 1 --iso-steps 0 --no-cpu-baseline --no-api "$@")
 
 run() {  # name, rocprofv3 args...
     local name=$1; shift

@@ -28,7 +28,9 @@ def main():
     ap.add_argument("--out")
     args = ap.parse_args()
     per, stats = pmc_summary.load(args.dir)
-    out = {"config": args.config, "panels": args.panels,
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench  # noqa: E402  (source_sha: the kernel sources these counters belong to)
+    out = {"config": args.config, "panels": args.panels, "source_sha": bench.source_sha(),
            "source": args.source or args.dir,
            "method": "rocprofv3 --pmc passes, one counter group per run (tools/gpu_prof.sh); FETCH_SIZE x2 "
                      "per MI355X_MICROARCH.md HBM section; WRITE_SIZE exact",
@@ -61,7 +63,11 @@ def main():
                 issue["lds_bank_conflict_per_active_lds"] = c.get("SQ_LDS_BANK_CONFLICT", 0) / c["SQ_ACTIVE_INST_LDS"]
             if c.get("SQ_WAVE_CYCLES"):
                 issue["wait_inst_any_frac"] = c.get("SQ_WAIT_INST_ANY", 0) / c["SQ_WAVE_CYCLES"]
+                issue["wait_any_frac"] = c.get("SQ_WAIT_ANY", 0) / c["SQ_WAVE_CYCLES"]
                 issue["active_inst_any_frac"] = c.get("SQ_ACTIVE_INST_ANY", 0) / c["SQ_WAVE_CYCLES"]
+                if gui:
+                    # occupancy: resident wave-cycles (SQ_WAVE_CYCLES counts quad-cycles) per SIMD-cycle
+                    issue["mean_waves_per_simd"] = 4 * c["SQ_WAVE_CYCLES"] / (SIMDS * gui / 8)
             issue["note"] = ("VALU issue fraction = SQ_INSTS_VALU x 2 cycles (wave64 on SIMD-32) / "
                              "(1024 SIMDs x GRBM_GUI_ACTIVE/8)")
             out["draw_issue"] = issue
