@@ -138,27 +138,39 @@ def cpu_baseline(inst_dir, k, seed, target_s, want_pairs):
     from oracle.legacy_oracle import read_instance
     d = os.path.join(REPO, "tests", "golden", "instances", inst_dir)
     o = read_instance(os.path.join(d, "categories.csv"), os.path.join(d, "respondents.csv"), k)
-    cores = len(os.sched_getaffinity(0))
+    visible = len(os.sched_getaffinity(0))
+    quota = cpu_quota()
+    # the CPU time this process may use: every visible core unless the cgroup caps it (cpu.max)
+    usable = max(1, min(visible, int(quota))) if quota else visible
 
-    def run(S):
+    def run(S, threads):
         t = time.perf_counter()
-        rc, panels, _, _ = coracle.draw(o, k, seed, 0, S, threads=cores)
+        rc, panels, _, _ = coracle.draw(o, k, seed, 0, S, threads=threads)
         assert rc == 0
         coracle.counts(panels, o.n)
         if want_pairs:
-            coracle.pairs(panels, o.n, threads=cores)
+            coracle.pairs(panels, o.n, threads=threads)
         coracle.unique(panels, o.n)
         return time.perf_counter() - t
 
-    probe = 4000
-    dt = run(probe)
-    S = int(min(max(probe, probe * target_s / max(dt, 1e-6)), 10 ** 7))
-    dt = run(S)
-    out = {"value": S / dt, "unit": "panels/s", "cores": cores, "kind": "port",
+    legs = {}
+    for threads in sorted({visible, usable}):
+        probe = 4000
+        dt = run(probe, threads)
+        S = int(min(max(probe, probe * target_s / max(dt, 1e-6)), 10 ** 7))
+        dt = run(S, threads)
+        legs[threads] = (S / dt, S, dt)
+    best = max(legs, key=lambda t: legs[t][0])
+    rate, S, dt = legs[best]
+    out = {"value": rate, "unit": "panels/s", "cores": best, "kind": "port",
            "sample": "%d panels of %s (draw+counts+%sunique), C oracle OpenMP x%d threads on %s" % (
-               S, inst_dir, "pairs+" if want_pairs else "", cores, cpu_model()),
-           "seconds": round(dt, 3), "cpu_model": cpu_model(), "host_cpus_affinity": cores,
-           "cgroup_cpu_quota": cpu_quota()}
+               S, inst_dir, "pairs+" if want_pairs else "", best, cpu_model()),
+           "seconds": round(dt, 3), "cpu_model": cpu_model(), "host_cpus_visible": visible,
+           "cgroup_cpu_quota": quota,
+           "port_by_threads": {str(t): {"panels_per_s": v[0], "panels": v[1], "seconds": round(v[2], 3)}
+                               for t, v in legs.items()},
+           "cores_note": "every visible host core was tried; the box's cgroup grants %s CPUs of time "
+                         "(cpu.max), so `cores` is the thread count that ran fastest" % quota}
     # Python restatement: probe, then ~target_s per process
     rate1, w1, _ = python_leg(d, k, seed, 20, 1)
     S1 = max(20, int(rate1 * target_s * 0.8))
@@ -166,11 +178,11 @@ def cpu_baseline(inst_dir, k, seed, target_s, want_pairs):
     out["python_1core"] = {"value": rate1, "unit": "panels/s", "cores": 1, "panels": S1, "seconds": round(w1, 3),
                            "sample": "oracle/legacy_oracle.py (Python restatement of analysis.py:162-191), 1 process"}
     Sp = max(10, int(rate1 * target_s * 0.5))
-    ratep, wp, innerp = python_leg(d, k, seed, Sp, cores)
-    out["python_per_core"] = {"value": ratep, "unit": "panels/s", "cores": cores, "panels_per_process": Sp,
+    ratep, wp, innerp = python_leg(d, k, seed, Sp, usable)
+    out["python_per_core"] = {"value": ratep, "unit": "panels/s", "cores": usable, "panels_per_process": Sp,
                               "seconds": round(wp, 3), "slowest_process_seconds": round(innerp, 3),
-                              "sample": "%d single-threaded Python processes (one per host core) of %d panels" % (
-                                  cores, Sp)}
+                              "sample": "%d single-threaded Python processes (one per usable host core) of %d "
+                                        "panels" % (usable, Sp)}
     out["reference_python_note"] = ("the unmodified reference (Python, dict + deepcopy) ran at 30.2 panels/s on one "
                                     "core at this shape (SURVEY.md section 6, dev container)")
     return out
@@ -268,9 +280,11 @@ def main():
     def Ev():
         return torch.cuda.Event(enable_timing=True)
 
+    mode = {"serial": not overlap}
+
     def enqueue_draw(j, rec):
         b = j % nb
-        ds = draw_stream
+        ds = stream if mode["serial"] else draw_stream
         ds.wait_event(counted[b])                 # step j - nb is done reading this buffer
         pipe.panels, pipe.hashes = pbufs[b], hbufs[b]
         begin = (j * world + rank) * S            # global panel indices, distinct per step and rank
@@ -371,10 +385,10 @@ def main():
     stage_pipe = stage_times(log)
     iso = {}
     if overlap and args.iso_steps:
-        ahead_saved = ahead
-        ahead = 0
+        torch.cuda.synchronize()
+        ahead_saved, ahead, mode["serial"] = ahead, 0, True     # every kernel alone, one stream
         run_steps(args.warmup + args.steps, args.iso_steps, iso)
-        ahead = ahead_saved
+        ahead, mode["serial"] = ahead_saved, False
         torch.cuda.synchronize()
         pipe.check_status()
     stage_ms = stage_times(iso) if iso else stage_pipe

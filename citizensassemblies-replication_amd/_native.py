@@ -12,6 +12,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(HERE)
 LIB_PATH = os.environ.get("CSA_LIB") or os.path.join(HERE, "libcsa_legacy.so")  # CSA_LIB: A/B builds
 SRC = os.path.join(HERE, "csrc", "csa_legacy.hip")
+SRC_MT = os.path.join(HERE, "csrc", "legacy_mt.cpp")   # host-only MT19937 mode
 HEADER = os.path.join(REPO, "include", "csa_legacy.h")
 
 CSA_OK = 0
@@ -50,6 +51,7 @@ SIGNATURES = {
     "csa_legacy_attempt": (ctypes.c_int, [_P, _I32, _U64, _U64, _U32, _P, _P, _P, _P, _P]),
     "csa_first_panel_not_in": (ctypes.c_int, [_P, _I32, _U64, _U64, _U64, _U32, _P, _U64, _U64, _P, _P]),
     "csa_draw_async": (ctypes.c_int, [_P, _I32, _U64, _U64, _U64, _U32, _P, _P, _P, _P, _P, _P]),
+    "csa_picks_stride": (_I32, [_I32]),
     "csa_draw_picks_supported": (ctypes.c_int, [_P, _I32]),
     "csa_draw_picks_async": (ctypes.c_int, [_P, _I32, _U64, _U64, _U64, _U32, _P, _P, _P, _P]),
     "csa_picks_pack_async": (ctypes.c_int, [_P, _U64, _I32, _I32, _P, _P, _P]),
@@ -66,6 +68,9 @@ SIGNATURES = {
     "csa_pairs_pack_async": (ctypes.c_int, [_P, _I32, _P, _P]),
     "csa_pairs_unpack_async": (ctypes.c_int, [_P, _I32, _P, _P]),
     "csa_status_decode": (ctypes.c_int, [_P]),
+    "csa_legacy_draw_mt": (ctypes.c_int, [_I32, _I32, _I32, _P, _P, _P, _P, _P, _P, _P, _I32, _P, _U64, _U32,
+                                          _I32, _P, _P, _P, _P, _P, _P]),
+    "csa_instance_set_address": (ctypes.c_int, [_P, _P]),
 }
 
 _lib = None
@@ -84,7 +89,7 @@ class CsaError(RuntimeError):
 def build(verbose=False):
     """Compile csrc/csa_legacy.hip for gfx950 into LIB_PATH (in-tree)."""
     cmd = ["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wall",
-           "-o", LIB_PATH, SRC]
+           "-o", LIB_PATH, SRC, SRC_MT]
     if verbose:
         print(" ".join(cmd))
     subprocess.check_call(cmd)

@@ -19,7 +19,14 @@ import numpy as np
 
 from . import _native as N
 from .instance import Instance, read_instance, encode, encode_cached, unpack_panel  # noqa: F401
-from .legacy import STREAM, seed, SelectionError, check_min_cats  # noqa: F401
+from . import legacy as _legacy
+from .legacy import STREAM, seed, SelectionError, check_min_cats, mt_draw  # noqa: F401
+
+
+def __getattr__(name):           # analysis.RNG_MODE follows legacy.RNG_MODE (set_rng_mode)
+    if name == "RNG_MODE":
+        return _legacy.RNG_MODE
+    raise AttributeError(name)
 
 ProbAllocation = Dict
 
@@ -169,25 +176,44 @@ class PanelSet:
         return set(self) == set(other)
 
 
-def legacy_find(feature_info, agents, k) -> List:
-    """analysis.py:141-159: one accepted panel, pick order, restarts on the device."""
-    enc = encode_cached(feature_info, agents)
-    k = int(k)
-    picks = np.full(max(k, 1), -1, np.int32)
-    first = STREAM.take_panels(1)
-    N.check(N.lib().csa_legacy_find(enc.handle, k, STREAM.key, first, 1, 0, N.ptr(picks), None))
-    return [enc.agent_ids[int(p)] for p in picks[:k] if p >= 0]
+def _with_address(enc, columns_data, check_same_address_columns):
+    """Same-address rings for the encoded agents (None without columns)."""
+    if columns_data is None or not check_same_address_columns:
+        return None
+    return _legacy.address_rings(enc.agent_ids, columns_data, check_same_address_columns)
 
 
-def legacy_find_batch(feature_info, agents, k, count, max_attempts=0):
+def legacy_find(feature_info, agents, k, rng: str = None, *, columns_data=None,
+                check_same_address_columns=None) -> List:
+    """analysis.py:141-159: one accepted panel, pick order, restarts on the device (Philox
+    stream) or, with rng="mt" (default: legacy.RNG_MODE), on the host from the stdlib random
+    stream as the reference consumes it.  With ``columns_data`` and
+    ``check_same_address_columns`` the draws delete same-address people (legacy.py:109-113;
+    the reference's legacy_find always passes check_same_address=False, analysis.py:150-151)."""
+    return legacy_find_batch(feature_info, agents, k, 1, rng=rng, columns_data=columns_data,
+                             check_same_address_columns=check_same_address_columns)[0]
+
+
+def legacy_find_batch(feature_info, agents, k, count, max_attempts=0, rng: str = None, *, columns_data=None,
+                      check_same_address_columns=None):
     """``count`` consecutive legacy_find calls in one launch (XMIN's caller, xmin.py:464-474)."""
     enc = encode_cached(feature_info, agents)
     k = int(k)
-    picks = np.full((int(count), max(k, 1)), -1, np.int32)
-    first = STREAM.take_panels(count)
-    N.check(N.lib().csa_legacy_find(enc.handle, k, STREAM.key, first, int(count), max_attempts,
-                                    N.ptr(picks), None))
+    ring = _with_address(enc, columns_data, check_same_address_columns)
     ids = enc.agent_ids
+    if (rng or _legacy.RNG_MODE) == "mt":
+        picks, _, _ = mt_draw(enc, k, int(count), max_attempts=max_attempts, addr_next=ring)
+        return [[ids[int(p)] for p in row[:k] if p >= 0] for row in picks]
+    picks = np.full((int(count), max(k, 1)), -1, np.int32)
+    L = N.lib()
+    first = STREAM.take_panels(count)
+    if ring is not None:
+        N.check(L.csa_instance_set_address(enc.handle, N.ptr(ring)))
+    try:
+        N.check(L.csa_legacy_find(enc.handle, k, STREAM.key, first, int(count), max_attempts, N.ptr(picks), None))
+    finally:
+        if ring is not None:
+            N.check(L.csa_instance_set_address(enc.handle, None))
     return [[ids[int(p)] for p in row[:k] if p >= 0] for row in picks]
 
 
@@ -223,13 +249,14 @@ def legacy_sample_raw(enc, k, iterations, random_seed, panel_begin=0, want_pairs
     return LegacyRaw(counts, pairs, int(unique[0]), panels, attempts)
 
 
-def legacy_sample_device(enc, k, S, random_seed, keep_panels=True, chunk=1 << 20):
+def legacy_sample_device(enc, k, S, random_seed, keep_panels=True, chunk=1 << 20, host_panels=None):
     """One legacy_probabilities batch on the device through a DevicePipeline cached with the
     encoding (picks / XT / scratch buffers reused across calls).  Panels and hashes of the whole
     batch go to fresh device tensors (the exact distinct count needs all of them; with
     ``keep_panels`` the returned PanelSet keeps the panel tensor and decodes it only when
     iterated).  Returns LegacyRaw with host counts and device pair counts (PairHistogram
-    materialises them lazily)."""
+    materialises them lazily).  ``host_panels`` (uint64[S, W], MT mode: drawn on the host)
+    replaces the device draw; the counting, pairs and distinct count still run on the device."""
     import torch
     from .device import DevicePipeline
     from .distributed import HashTable
@@ -251,7 +278,12 @@ def legacy_sample_device(enc, k, S, random_seed, keep_panels=True, chunk=1 << 20
             for off in range(0, S, C):
                 ln = min(C, S - off)
                 pipe.panels, pipe.hashes = panels[off * W:(off + ln) * W], hashes[2 * off:2 * (off + ln)]
-                pipe.draw(random_seed, off, ln)
+                if host_panels is None:
+                    pipe.draw(random_seed, off, ln)
+                else:
+                    src = np.ascontiguousarray(host_panels[off:off + ln], np.uint64).view(np.int64).reshape(-1)
+                    pipe.panels.copy_(torch.from_numpy(src), non_blocking=False)
+                    pipe.hash(ln)
                 pipe.transpose_count(ln)
                 pipe.pair_counts(ln, overwrite=off == 0)
             if S == 0:
@@ -273,21 +305,38 @@ def legacy_sample_device(enc, k, S, random_seed, keep_panels=True, chunk=1 << 20
 
 
 def legacy_probabilities(instance: Instance, iterations: int, random_seed: int,
-                         keep_panels: bool = True) -> Tuple[ProbAllocation, PanelSet, PairHistogram]:
+                         keep_panels: bool = True, rng: str = None) -> Tuple[ProbAllocation, PanelSet, PairHistogram]:
     """analysis.py:162-191 on the GPU.
 
     Returns ``({agent_id: count/S}, found_panels, pair_histogram)`` with the
     pair histogram divided by S, as the reference.  With torch.distributed
     initialised and world size > 1 the panels are sharded over ranks (see
     ``distributed.legacy_probabilities_distributed``).
+
+    ``rng="mt"`` (default: ``legacy.RNG_MODE``) reproduces the reference's own
+    stream: ``random.seed(random_seed)`` (analysis.py:169), then the panels are
+    drawn on the host from the stdlib MT19937 state exactly as legacy.py:149
+    consumes it (csa_legacy_draw_mt) and counted / paired / deduplicated on the
+    device.  It matches the published reference_output probabilities.
     """
     from . import distributed as D
+    mode = rng or _legacy.RNG_MODE
+    if mode not in ("philox", "mt"):
+        raise ValueError("rng must be 'philox' or 'mt'")
+    enc = encode_cached(instance.categories, instance.agents)
+    S = int(iterations)
+    if mode == "mt":
+        import random
+        random.seed(random_seed)
+        np.random.seed(random_seed)                  # analysis.py:170 (unused by LEGACY)
+        enc.check_quotas(instance.k)
+        picks, panels, _ = mt_draw(enc, instance.k, S)
+        raw = legacy_sample_device(enc, instance.k, S, random_seed, keep_panels=keep_panels, host_panels=panels)
+        return finish(instance, enc, raw, S)
     if D.world_size() > 1:
         return D.legacy_probabilities_distributed(instance, iterations, random_seed, keep_panels=keep_panels)
     seed(random_seed)
-    enc = encode_cached(instance.categories, instance.agents)
     enc.check_quotas(instance.k)
-    S = int(iterations)
     STREAM.take_panels(S)
     raw = legacy_sample_device(enc, instance.k, S, random_seed, keep_panels=keep_panels)
     return finish(instance, enc, raw, S)

@@ -120,6 +120,7 @@ struct DrawArgs {
     const int32_t *fmin, *fmax, *sel0, *rem0;
     const uint64_t *present0;  // W
     const uint32_t *pmask;     // n person feature masks (bit f = holds feature f; F <= 32) or null
+    const int32_t *addr_next;  // same-address rings (check_same_address, draw_kernel GENERAL) or null
     int32_t n, F, W, Ws, k;
     uint32_t max_attempts, attempt_base;
     int32_t single;            // 1: exactly one attempt, no min-quota check, write final state
@@ -411,6 +412,29 @@ __global__ __launch_bounds__(draw_threads(FPL, WPL), draw_occupancy(FPL, WPL)) v
                             const uint64_t b = (glane * WPL + j == wi) ? bit : 0ull;
                             rmn[j] &= ~b;
                             pk[j] |= b;
+                        }
+                        // check_same_address (legacy.py:109-113): the remaining agents at the
+                        // pick's address are deleted with selected=False before the cascades
+                        // (walk of the pick's address ring; uniform across the group)
+                        if constexpr (GENERAL) {
+                            if (A.addr_next) {
+                                for (int q = A.addr_next[p], guard = 0; q != p && guard < A.n;
+                                     q = A.addr_next[q], ++guard) {
+                                    const int wq = q >> 6, bq = q & 63;
+                                    bool there = false;
+#pragma unroll
+                                    for (int j = 0; j < WPL; ++j)
+                                        if (glane * WPL + j == wq) there = (rmn[j] >> bq) & 1ull;
+                                    if (group_any<G>(there, gbase)) {
+#pragma unroll
+                                        for (int j = 0; j < WPL; ++j)
+                                            if (glane * WPL + j == wq) rmn[j] &= ~(1ull << bq);
+#pragma unroll
+                                        for (int j = 0; j < FPL; ++j)
+                                            rem[j] -= (int)((fm32[2 * (fid[j] * Ls + wq) + (bq >> 5)] >> (bq & 31)) & 1u);
+                                    }
+                                }
+                            }
                         }
                         // delete_all_in_cat for every full feature of the pick (legacy.py:47-62,
                         // 115-119), bulk form D = remaining & OR(featmask[full])
@@ -1142,6 +1166,9 @@ __global__ __launch_bounds__(256) void pair_histogram_lds_kernel(const int64_t *
 
 }  // namespace
 
+// library-internal: lets legacy_mt.cpp set the csa_last_error() message
+void csa_set_last_error(const char *msg) { g_err = msg ? msg : ""; }
+
 // ==========================================================================================
 // Host side
 // ==========================================================================================
@@ -1155,6 +1182,7 @@ struct csa_instance {
     int32_t *d_fmin = nullptr, *d_fmax = nullptr, *d_sel0 = nullptr, *d_rem0 = nullptr;
     uint64_t *d_present0 = nullptr;
     uint32_t *d_pmask = nullptr;  // n person feature masks (F <= 32 only)
+    int32_t *d_addr_next = nullptr;  // same-address rings (csa_instance_set_address) or null
     int32_t max_abs = 0;  // max |fmin| / |sel0| bound for the cross-multiplication range check
     bool zero_max_min = false;  // some feature has max 0 and min > 0 (draw_batch_kernel excludes it)
     bool sel_over_max = false;  // some feature starts with selected > max (draw_lane_kernel excludes it)
@@ -1278,6 +1306,7 @@ int pow2_ceil_int(int x) {
 // single-attempt draws (general mode) use draw_kernel<64, ..., true>.  CSA_DRAW_KERNEL=lane|16|64
 // forces a batch kernel the instance fits (parity tests of every layout).
 int pick_draw_config(const csa_instance *I, bool general, DrawConfig &c) {
+    general = general || I->d_addr_next;  // same-address deletions: draw_kernel<64, ..., true> only
     const bool lane_ok = I->F <= 32 && I->d_pmask && !I->zero_max_min && I->W <= 32 && I->max_abs < 32768 &&
                          !I->sel_over_max;
     const bool g16_ok = I->F <= 64 && I->W <= 256;
@@ -1393,6 +1422,7 @@ int launch_draw(const csa_instance *I, int32_t k, uint64_t seed, uint64_t panel_
     A.rem0 = I->d_rem0;
     A.present0 = I->d_present0;
     A.pmask = I->d_pmask;
+    A.addr_next = I->d_addr_next;
     A.n = I->n;
     A.F = I->F;
     A.W = I->W;
@@ -1417,7 +1447,7 @@ int launch_draw(const csa_instance *I, int32_t k, uint64_t seed, uint64_t panel_
     csa_instance *M = const_cast<csa_instance *>(I);  // the lane kernel's pick-list scratch
     if (d_picks_ext)
         A.picks16 = d_picks_ext;
-    else if (cfg.lane && (rc = lane_picks(M, n_panels * (uint64_t)k, stream, &A.picks16)))
+    else if (cfg.lane && (rc = lane_picks(M, n_panels * (uint64_t)((k + 7) & ~7), stream, &A.picks16)))
         return rc;
     const int threads = cfg.lane ? kLaneThreads : draw_threads(cfg.FPL, cfg.WPL);
     const int groups_wg = threads / cfg.G;
@@ -1591,6 +1621,7 @@ void csa_instance_destroy(csa_instance *I) {
     if (I->d_rem0) (void)hipFree(I->d_rem0);
     if (I->d_present0) (void)hipFree(I->d_present0);
     if (I->d_pmask) (void)hipFree(I->d_pmask);
+    if (I->d_addr_next) (void)hipFree(I->d_addr_next);
     if (I->sdraw) (void)hipStreamSynchronize(I->sdraw);
     if (I->spost) (void)hipStreamSynchronize(I->spost);
     for (int i = 0; i < 16; ++i)
@@ -1636,6 +1667,25 @@ int csa_instance_set_state(csa_instance *I, const int32_t *sel, const int32_t *r
     I->sel0.assign(sel ? sel : zeros.data(), (sel ? sel : zeros.data()) + I->F);
     HIPCHK(hipMemcpy(I->d_rem0, rem ? rem : I->pool.data(), I->F * 4, hipMemcpyHostToDevice));
     if (I->W) HIPCHK(hipMemcpy(I->d_present0, present ? present : all.data(), I->W * 8, hipMemcpyHostToDevice));
+    return CSA_OK;
+}
+
+int csa_instance_set_address(csa_instance *I, const int32_t *addr_next) {
+    if (!I) return fail(CSA_E_INVALID, "null instance");
+    ScopedDevice sd(I->device);
+    if (I->picks_pending) HIPCHK(hipEventSynchronize(I->picks_done));
+    if (!addr_next) {
+        if (I->d_addr_next) HIPCHK(hipFree(I->d_addr_next));
+        I->d_addr_next = nullptr;
+        return CSA_OK;
+    }
+    for (int p = 0; p < I->n; ++p)
+        if (addr_next[p] < 0 || addr_next[p] >= I->n) return fail(CSA_E_INVALID, "addr_next[%d] out of range", p);
+    if (!I->d_addr_next) {
+        int rc = dalloc(&I->d_addr_next, (size_t)I->n);
+        if (rc) return rc;
+    }
+    HIPCHK(hipMemcpy(I->d_addr_next, addr_next, (size_t)I->n * 4, hipMemcpyHostToDevice));
     return CSA_OK;
 }
 
@@ -1726,6 +1776,8 @@ int csa_draw_async(const csa_instance *I, int32_t k, uint64_t seed, uint64_t pan
     return launch_draw(I, k, seed, panel_begin, n_panels, max_attempts, 0, 0, d_panels, d_hashes, d_attempts,
                        d_picks, d_status, nullptr, nullptr, nullptr, (hipStream_t)stream);
 }
+
+int32_t csa_picks_stride(int32_t k) { return (k + 7) & ~7; }
 
 int csa_draw_picks_supported(const csa_instance *I, int32_t k) {
     if (!I || check_k(I, k)) return 0;

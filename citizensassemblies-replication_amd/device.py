@@ -52,7 +52,8 @@ class DevicePipeline:
             _ = enc.handle  # upload the instance on this device
             # the lane kernel writes pick lists (u16) that picks_pack_kernel packs; others write bitmasks
             self.split_draw = bool(L.csa_draw_picks_supported(enc.handle, self.k)) and self.k > 0
-            self.picks = torch.empty(max(S * self.k, 1), dtype=torch.int16, device=dev) if self.split_draw else None
+            self.kpad = int(L.csa_picks_stride(self.k))
+            self.picks = torch.empty(max(S * self.kpad, 1), dtype=torch.int16, device=dev) if self.split_draw else None
             self.panels = torch.empty(S * W, dtype=u64, device=dev)
             self.hashes = torch.empty(2 * S, dtype=u64, device=dev) if want_unique else None
             self.attempts = torch.empty(S, dtype=torch.int32, device=dev) if want_attempts else None

@@ -64,7 +64,7 @@ class EncodedInstance:
                 fmax.append(int(info["max"]))
                 fcat.append(c)
                 sel.append(int(info.get("selected", 0)))
-                rem.append(int(info.get("remaining", 0)))
+                rem.append(int(info["remaining"]) if "remaining" in info else -1)   # -1: the pool count
         self.agent_ids = list(agents)
         self.n = len(self.agent_ids)
         self.C = len(self.cat_names)
@@ -83,6 +83,7 @@ class EncodedInstance:
         self.rem0 = np.asarray(rem, np.int32)
         self.pool = np.bincount(pf.ravel(), minlength=self.F).astype(np.int32) if self.n else \
             np.zeros(self.F, np.int32)
+        self.rem0 = np.where(self.rem0 < 0, self.pool, self.rem0).astype(np.int32)
         self._handle = None
 
     # -- native handle ---------------------------------------------------------------------

@@ -73,6 +73,14 @@ int csa_instance_info(const csa_instance *inst, int32_t *n, int32_t *C, int32_t 
 int csa_instance_set_state(csa_instance *inst, const int32_t *sel, const int32_t *rem,
                            const uint64_t *present);
 
+/* check_same_address (legacy.py:78-99, 103-113): addr_next (n int32) links the agents that share
+ * an address (the check_same_address_columns values) into rings, agent order: addr_next[p] = the
+ * next agent at p's address, p itself when p lives alone.  With a ring set, every pick deletes
+ * the remaining agents at its address (really_delete_person(selected=False)) before the
+ * full-category cascades; all draws of the instance then run draw_kernel<64, ..., true>.
+ * NULL removes the rings (the default: the reference harness passes False, analysis.py:150). */
+int csa_instance_set_address(csa_instance *inst, const int32_t *addr_next);
+
 /* ---- host-buffer API (blocking) ------------------------------------------ */
 
 /* legacy_probabilities (analysis.py:162-191) for panels
@@ -119,6 +127,22 @@ int csa_first_panel_not_in(csa_instance *inst, int32_t k, uint64_t seed, uint64_
                            uint64_t n_panels, uint32_t max_attempts, const uint64_t *portfolio,
                            uint64_t m, uint64_t chunk, int64_t *index_out, uint64_t *panel_out);
 
+/* MT19937 mode (the reference's own stream), host only, no device
+ * needed: `n_panels` consecutive legacy_find calls (analysis.py:141-159; single = 1: ONE
+ * find_random_sample_legacy call, legacy.py:178-200, returning CSA_E_SELECTION on a dead end)
+ * drawing from the stdlib random stream exactly as legacy.py:149 consumes it.  mt_state: 625
+ * uint32 = CPython's random.getstate()[1] (624 words + position), advanced in place.  Instance
+ * arrays as csa_instance_create; sel0 / rem0 (F) and present0 (W) give the start state (NULL =
+ * 0 / pool counts / everyone), addr_next the same-address rings (or NULL, see
+ * csa_instance_set_address).  Outputs (each may be NULL): picks_out n_panels*k (pick order, -1
+ * padded), panels_out n_panels*W, attempts_out n_panels; with single, the final sel/rem (F) and
+ * remaining pool (W). */
+int csa_legacy_draw_mt(int32_t n, int32_t C, int32_t F, const int32_t *person_feat, const int32_t *fmin,
+                       const int32_t *fmax, const int32_t *sel0, const int32_t *rem0, const uint64_t *present0,
+                       const int32_t *addr_next, int32_t k, uint32_t *mt_state, uint64_t n_panels,
+                       uint32_t max_attempts, int32_t single, int32_t *picks_out, uint64_t *panels_out,
+                       uint32_t *attempts_out, int32_t *sel_out, int32_t *rem_out, uint64_t *present_out);
+
 /* ---- stream-ordered device API ---------------------------------------------
  * All buffers are device pointers on the instance's device; `stream` is a
  * hipStream_t (NULL = default stream).  Nothing synchronises; errors inside
@@ -137,10 +161,13 @@ int csa_draw_async(const csa_instance *inst, int32_t k, uint64_t seed, uint64_t 
 /* The same draw split in two, for instances whose batch draw is the pick-list kernel
  * (draw_lane_kernel: F <= 32, n <= 2048; csa_draw_picks_supported returns 1 for them, else 0 and
  * csa_draw_picks_async returns CSA_E_UNSUPPORTED).  csa_draw_picks_async writes each panel's k
- * picks in pick order (d_picks: n_panels*k uint16; legacy.py:194 people_selected order);
+ * picks in pick order (legacy.py:194 people_selected order) into a row of
+ * csa_picks_stride(k) = k rounded up to 8 uint16 (d_picks: n_panels * stride; entries past k
+ * unspecified);
  * csa_picks_pack_async turns pick lists into packed panels (n_panels*W) and, if d_hashes is not
  * NULL, their 128-bit hashes.  csa_draw_async = the two back to back on one stream (with an
  * instance-owned pick buffer: concurrent csa_draw_async calls on one instance serialise). */
+int32_t csa_picks_stride(int32_t k);
 int csa_draw_picks_supported(const csa_instance *inst, int32_t k);
 int csa_draw_picks_async(const csa_instance *inst, int32_t k, uint64_t seed, uint64_t panel_begin,
                          uint64_t n_panels, uint32_t max_attempts, uint16_t *d_picks, uint32_t *d_attempts,

@@ -104,7 +104,8 @@ def test_pick_lists_match_oracle_pick_order(gpu_available, name, k, S, seed):
     enc = P.encode(inst.categories, inst.agents)
     assert N.lib().csa_draw_picks_supported(enc.handle, k) == 1
     begin = 4242
-    picks = torch.empty(S * k, dtype=torch.int16, device="cuda")
+    kp = int(N.lib().csa_picks_stride(k))
+    picks = torch.empty(S * kp, dtype=torch.int16, device="cuda")
     att = torch.empty(S, dtype=torch.int32, device="cuda")
     status = torch.zeros(4, dtype=torch.int32, device="cuda")
     N.check(N.lib().csa_draw_picks_async(enc.handle, k, seed, begin, S, 0, N.ptr(picks), N.ptr(att), N.ptr(status),
@@ -117,7 +118,7 @@ def test_pick_lists_match_oracle_pick_order(gpu_available, name, k, S, seed):
     o = oracle_read(*inst_paths(name), k)
     rc, opanels, oatt, opicks = coracle.draw(o, k, seed, begin, S, want_picks=True)
     assert rc == 0
-    assert np.array_equal(picks.cpu().numpy().astype(np.int32).reshape(S, k), opicks)
+    assert np.array_equal(picks.cpu().numpy().astype(np.int32).reshape(S, kp)[:, :k], opicks)
     assert np.array_equal(att.cpu().numpy().astype(np.uint32), oatt)
     got = panels.cpu().numpy().view(np.uint64).reshape(S, enc.W)
     assert np.array_equal(got, opanels)
@@ -133,10 +134,12 @@ def test_picks_pack_edges(gpu_available, S):
     D = pkg("distributed")
     rng = np.random.default_rng(S)
     for n, k in ((200, 7), (1727, 110), (64, 1), (2048, 33)):
-        picks = np.stack([rng.choice(n, size=k, replace=False) for _ in range(S)]).astype(np.int16)
+        kp = int(N.lib().csa_picks_stride(k))
+        picks = np.full((S, kp), -1, np.int16)          # entries past k are ignored
+        picks[:, :k] = np.stack([rng.choice(n, size=k, replace=False) for _ in range(S)])
         want = np.zeros((S, (n + 63) // 64), np.uint64)
         for i in range(S):
-            for p in picks[i].astype(np.int64):
+            for p in picks[i, :k].astype(np.int64):
                 want[i, p >> 6] |= np.uint64(1) << np.uint64(p & 63)
         d = torch.from_numpy(picks.ravel().copy()).cuda()
         W = (n + 63) // 64

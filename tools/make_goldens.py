@@ -175,6 +175,103 @@ def run_case(legacy, analysis, case, inst_dir, k, S, seed):
     return g
 
 
+# check_same_address cases (legacy.py:78-99, 103-113): the reference harness never sets the flag
+# (analysis.py:150-151), so these drive find_random_sample_legacy directly in a legacy_find-shaped
+# restart loop (deepcopy, SelectionError -> next attempt, check_min_cats -> next attempt), with an
+# address column committed next to the instance.  (case, instance dir, k, S, seed)
+ADDRESS_CASES = [
+    ("address_example_small_20_s2", "example_small_20", 20, 2000, 2),
+    ("address_sf_e_tight_110_s1", "sf_e_tight_110", 110, 150, 1),
+]
+ADDR_COLS = ["primary_address1", "primary_zip"]
+
+
+def write_addresses(inst_dir, n, seed=0):
+    """Synthetic households: sizes 1-4 (40/30/20/10 %), members in shuffled agent order; the street
+    part repeats across zip codes, so equal address1 alone is not the same address."""
+    path = os.path.join(INST, inst_dir, "addresses.csv")
+    if os.path.exists(path):
+        return path
+    rng = np.random.default_rng(seed)
+    order = rng.permutation(n)
+    rows = [None] * n
+    h = i = 0
+    while i < n:
+        size = int(rng.choice([1, 2, 3, 4], p=[0.4, 0.3, 0.2, 0.1]))
+        street = "%d Main St" % (h % max(4, n // 16))
+        zipc = "Z%03d" % (h % 37)
+        for p in order[i:i + size]:
+            rows[p] = (street, zipc)
+        i += size
+        h += 1
+    with open(path, "w", newline="", encoding="utf-8") as fh:
+        w = csv.writer(fh)
+        w.writerow(ADDR_COLS)
+        w.writerows(rows)
+    return path
+
+
+def read_addresses(path):
+    with open(path, encoding="utf-8") as fh:
+        return {i: dict(r) for i, r in enumerate(csv.DictReader(fh))}
+
+
+def address_case(legacy, analysis, case, inst_dir, k, S, seed, mode):
+    import copy
+    import random
+    d = os.path.join(INST, inst_dir)
+    inst = analysis.read_instance(os.path.join(d, "categories.csv"), os.path.join(d, "respondents.csv"), k)
+    n = len(inst.agents)
+    columns_data = read_addresses(write_addresses(inst_dir, n))
+    picks, attempts, single = [], [], []
+    harness = PhiloxHarness(legacy, analysis, seed) if mode == "philox" else None
+    if harness:
+        harness.__enter__()
+    else:
+        random.seed(seed)
+    t0 = time.time()
+    try:
+        for i in range(S):
+            a = -1
+            while True:
+                a += 1
+                cats, people = copy.deepcopy(inst.categories), copy.deepcopy(inst.agents)
+                if harness:
+                    harness.panel, harness.attempt, harness.step = i, a, 0
+                rec = {"panel": i, "attempt": a}
+                try:
+                    sel, lines = legacy.find_random_sample_legacy(cats, people, columns_data, k, True, ADDR_COLS)
+                except legacy.SelectionError:
+                    if len(single) < 40:
+                        single.append(dict(rec, status="SelectionError"))
+                    continue
+                ok, _ = legacy.check_min_cats(cats)
+                if len(single) < 40:
+                    single.append(dict(rec, status="ok", picks=list(sel), lines=lines,
+                                       selected=[[c, f, v["selected"], v["remaining"]] for c in cats
+                                                 for f, v in cats[c].items()],
+                                       people_left=sorted(people)))
+                if not ok:
+                    continue
+                picks.append(list(sel))
+                attempts.append(a + 1)
+                break
+    finally:
+        if harness:
+            harness.__exit__(None, None, None)
+    panels = [tuple(sorted(p)) for p in picks]
+    counts = np.zeros(n, np.int64)
+    for p in panels:
+        counts[list(p)] += 1
+    return {"case": case, "instance": inst_dir, "k": k, "S": S, "seed": seed, "n": n, "rng": mode,
+            "columns": ADDR_COLS, "addresses": "tests/golden/instances/%s/addresses.csv" % inst_dir,
+            "generator": "tools/make_goldens.py driving the unmodified reference's find_random_sample_legacy "
+                         "with check_same_address=True in a legacy_find-shaped restart loop",
+            "reference_seconds": round(time.time() - t0, 3), "counts": counts.tolist(),
+            "unique": len(set(panels)), "attempts": attempts, "panels_sha256": sha(pack(panels, n)),
+            "picks": picks if S * k <= 50000 else picks[:200], "single_attempts": single}
+
+
 def mt_goldens():
     out = {}
     for name, k, rel in (
@@ -213,6 +310,15 @@ def main(argv):
     if not want or "mt" in want:
         with open(os.path.join(GOLD, "mt_published.json"), "w") as fh:
             json.dump(mt_goldens(), fh, separators=(",", ":"))
+    for case, inst_dir, k, S, seed in ADDRESS_CASES:
+        if want and case not in want and "address" not in want:
+            continue
+        g = {mode: address_case(legacy, analysis, case, inst_dir, k, S, seed, mode) for mode in ("philox", "mt")}
+        with open(os.path.join(GOLD, "%s.json" % case), "w") as fh:
+            json.dump(g, fh, separators=(",", ":"))
+        print("%-28s philox unique=%d attempts=%d  mt unique=%d attempts=%d" % (
+            case, g["philox"]["unique"], sum(g["philox"]["attempts"]), g["mt"]["unique"],
+            sum(g["mt"]["attempts"])), file=sys.stderr)
 
 
 if __name__ == "__main__":
