@@ -1188,8 +1188,8 @@ struct csa_instance {
     bool sel_over_max = false;  // some feature starts with selected > max (draw_lane_kernel excludes it)
     // grow-only device scratch + a stream for the repeated small host-API calls
     // (csa_first_panel_not_in: XMIN calls it 5n times)
-    void *scratch[16] = {};   // slots 0-7: csa_first_panel_not_in; 8-15: csa_legacy_sample
-    size_t scratch_bytes[16] = {};
+    void *scratch[24] = {};   // slots 0-7: csa_first_panel_not_in; 8-23: csa_legacy_sample
+    size_t scratch_bytes[24] = {};
     hipStream_t stream = nullptr;
     hipStream_t sdraw = nullptr, spost = nullptr;  // csa_legacy_sample's pipeline
     hipEvent_t drawn = nullptr;
@@ -1484,7 +1484,7 @@ int read_status(const uint32_t *d_status, hipStream_t stream, uint32_t *h) {
 
 // csa_legacy_sample's pipeline chunk (panels): 2^20 = one bench step at sf_e
 constexpr uint64_t kSampleChunk = 1ull << 20;
-constexpr int kSampleSlot0 = 8, kScratchSlots = 16;          // instance scratch slots of csa_legacy_sample
+constexpr int kSampleSlot0 = 8, kScratchSlots = 24;          // instance scratch slots of csa_legacy_sample
 constexpr size_t kSampleKeepBytes = (size_t)8 << 30;          // kept across calls up to 8 GiB
 
 uint64_t pow2_at_least(uint64_t x) {
@@ -1504,6 +1504,7 @@ struct DevBuf {
 // instance scratch slot `slot` with at least `count` elements (grow-only)
 template <typename T>
 int scratch(csa_instance *I, int slot, size_t count, T **out) {
+    if (slot < 0 || slot >= kScratchSlots) return fail(CSA_E_INVALID, "internal: scratch slot %d", slot);
     const size_t bytes = std::max<size_t>(count, 1) * sizeof(T);
     if (I->scratch_bytes[slot] < bytes) {
         if (I->scratch[slot]) HIPCHK(hipFree(I->scratch[slot]));
@@ -1614,6 +1615,11 @@ int csa_instance_create(int32_t n, int32_t C, int32_t F, const int32_t *person_f
 void csa_instance_destroy(csa_instance *I) {
     if (!I) return;
     ScopedDevice sd(I->device);
+    // drain everything that may still use the instance's buffers, while its streams exist
+    if (I->picks_done && I->picks_pending) (void)hipEventSynchronize(I->picks_done);
+    if (I->sdraw) (void)hipStreamSynchronize(I->sdraw);
+    if (I->spost) (void)hipStreamSynchronize(I->spost);
+    if (I->stream) (void)hipStreamSynchronize(I->stream);
     if (I->d_featmask) (void)hipFree(I->d_featmask);
     if (I->d_fmin) (void)hipFree(I->d_fmin);
     if (I->d_fmax) (void)hipFree(I->d_fmax);
@@ -1622,17 +1628,14 @@ void csa_instance_destroy(csa_instance *I) {
     if (I->d_present0) (void)hipFree(I->d_present0);
     if (I->d_pmask) (void)hipFree(I->d_pmask);
     if (I->d_addr_next) (void)hipFree(I->d_addr_next);
-    if (I->sdraw) (void)hipStreamSynchronize(I->sdraw);
-    if (I->spost) (void)hipStreamSynchronize(I->spost);
-    for (int i = 0; i < 16; ++i)
+    if (I->d_picks16) (void)hipFree(I->d_picks16);
+    for (int i = 0; i < kScratchSlots; ++i)
         if (I->scratch[i]) (void)hipFree(I->scratch[i]);
+    if (I->picks_done) (void)hipEventDestroy(I->picks_done);
+    if (I->drawn) (void)hipEventDestroy(I->drawn);
     if (I->stream) (void)hipStreamDestroy(I->stream);
     if (I->sdraw) (void)hipStreamDestroy(I->sdraw);
     if (I->spost) (void)hipStreamDestroy(I->spost);
-    if (I->drawn) (void)hipEventDestroy(I->drawn);
-    if (I->picks_done) (void)hipEventSynchronize(I->picks_done);
-    if (I->d_picks16) (void)hipFree(I->d_picks16);
-    if (I->picks_done) (void)hipEventDestroy(I->picks_done);
     delete I;
 }
 
