@@ -559,6 +559,7 @@ __global__ __launch_bounds__(draw_threads(FPL, WPL), draw_occupancy(FPL, WPL)) v
 }
 
 #include "draw_lane.inc"
+#include "draw_wide.inc"
 
 // 128-bit panel hashes (the draw_kernel's in-kernel hash, for the batch kernel's panels): a
 // quad of lanes per panel, words glane, glane+4, ... (coalesced within the quad), quad sum.
@@ -1231,8 +1232,30 @@ int check_k(const csa_instance *I, int32_t k) {
 struct DrawConfig {
     int G = 16, FPL = 1, WPL = 1;
     bool lane = false;  // draw_lane_kernel (2 lanes per panel): FPL / WPL hold its FN / WN
+    bool wide = false;  // draw_wide_kernel (8 lanes per panel)
     const void *fn = nullptr;
+    bool picks() const { return lane || wide; }  // pick-list kernels (picks_pack_kernel builds the panels)
 };
+
+template <int FPL>
+const void *wide_fn_w(int wpl) {
+    switch (wpl) {
+        case 4: return reinterpret_cast<const void *>(&draw_wide_kernel<8, FPL, 4>);
+        case 8: return reinterpret_cast<const void *>(&draw_wide_kernel<8, FPL, 8>);
+        case 16: return reinterpret_cast<const void *>(&draw_wide_kernel<8, FPL, 16>);
+        default: return nullptr;
+    }
+}
+
+const void *wide_fn(int fpl, int wpl) {
+    switch (fpl) {
+        case 2: return wide_fn_w<2>(wpl);
+        case 4: return wide_fn_w<4>(wpl);
+        case 5: return wide_fn_w<5>(wpl);
+        case 8: return wide_fn_w<8>(wpl);
+        default: return nullptr;
+    }
+}
 
 // holder-scan batch of the lane kernel: all of a lane's row words in one LDS round trip
 // (CSA_LANE_SKDIV > 1 splits them, trading a round trip for VGPRs)
@@ -1309,14 +1332,25 @@ int pick_draw_config(const csa_instance *I, bool general, DrawConfig &c) {
     general = general || I->d_addr_next;  // same-address deletions: draw_kernel<64, ..., true> only
     const bool lane_ok = I->F <= 32 && I->d_pmask && !I->zero_max_min && I->W <= 32 && I->max_abs < 32768 &&
                          !I->sel_over_max;
+    const bool wide_ok = I->F <= 64 && I->W <= 128 && !I->zero_max_min && I->max_abs < 32768 && !I->sel_over_max;
     const bool g16_ok = I->F <= 64 && I->W <= 256;
-    int choice = general ? 64 : lane_ok ? 2 : g16_ok ? 16 : 64;
+    int choice = general ? 64 : lane_ok ? 2 : wide_ok ? 8 : g16_ok ? 16 : 64;
     if (const char *e = getenv("CSA_DRAW_KERNEL")) {
         if (!general && !strcmp(e, "lane") && lane_ok) choice = 2;
+        else if (!general && !strcmp(e, "wide") && wide_ok) choice = 8;
         else if (!general && !strcmp(e, "16") && g16_ok) choice = 16;
         else if (!general && !strcmp(e, "64")) choice = 64;
     }
     c.G = choice;
+    if (choice == 8) {  // draw_wide_kernel: FPL in {2, 4, 5, 8}, WPL in {4, 8, 16}
+        const int fpl = (I->F + 7) / 8;
+        c.wide = true;
+        c.FPL = fpl <= 2 ? 2 : fpl <= 4 ? 4 : fpl <= 5 ? 5 : 8;
+        c.WPL = I->W <= 32 ? 4 : I->W <= 64 ? 8 : 16;
+        c.fn = wide_fn(c.FPL, c.WPL);
+        if (!c.fn) return fail(CSA_E_UNSUPPORTED, "no wide draw kernel for F=%d W=%d", I->F, I->W);
+        return CSA_OK;
+    }
     if (choice == 2) {
         c.lane = true;
         c.FPL = std::max(8, pow2_ceil_int(I->F));
@@ -1443,23 +1477,24 @@ int launch_draw(const csa_instance *I, int32_t k, uint64_t seed, uint64_t panel_
     A.sel_out = d_sel_out;
     A.rem_out = d_rem_out;
     A.present_out = d_present_out;
-    if (d_picks_ext && !cfg.lane) return fail(CSA_E_UNSUPPORTED, "this instance does not take the pick-list draw");
+    if (d_picks_ext && !cfg.picks()) return fail(CSA_E_UNSUPPORTED, "this instance does not take the pick-list draw");
     csa_instance *M = const_cast<csa_instance *>(I);  // the lane kernel's pick-list scratch
     if (d_picks_ext)
         A.picks16 = d_picks_ext;
-    else if (cfg.lane && (rc = lane_picks(M, n_panels * (uint64_t)((k + 7) & ~7), stream, &A.picks16)))
+    else if (cfg.picks() && (rc = lane_picks(M, n_panels * (uint64_t)((k + 7) & ~7), stream, &A.picks16)))
         return rc;
-    const int threads = cfg.lane ? kLaneThreads : draw_threads(cfg.FPL, cfg.WPL);
+    const int threads = cfg.lane ? kLaneThreads : cfg.wide ? kWideThreads : draw_threads(cfg.FPL, cfg.WPL);
     const int groups_wg = threads / cfg.G;
-    const size_t lds = cfg.lane ? lane_lds_bytes(cfg.FPL, cfg.WPL, I->n)
-                                : draw_lds_bytes(cfg.G, cfg.FPL, cfg.WPL, I->W, k, groups_wg);
+    const size_t lds = cfg.lane   ? lane_lds_bytes(cfg.FPL, cfg.WPL, I->n)
+                       : cfg.wide ? wide_lds_bytes(cfg.G, cfg.FPL, cfg.WPL)
+                                  : draw_lds_bytes(cfg.G, cfg.FPL, cfg.WPL, I->W, k, groups_wg);
     if (lds > 160 * 1024) return fail(CSA_E_UNSUPPORTED, "draw kernel needs %zu B of LDS", lds);
     const uint64_t want = (n_panels + groups_wg - 1) / groups_wg;
     // the lane kernel: one workgroup per 128 panels, not persistent -- sf_e 10^6 panels: 4.47 ms vs
     // 5.05 ms for a persistent grid, and retiring workgroups let a concurrent stream's kernels in.
     // draw_kernel: one resident grid (its 66 KB of feature rows at n = 8192 load once per workgroup)
     uint64_t grid = want;
-    if (!cfg.lane) {
+    if (!cfg.picks()) {
         int per_cu = 0, cus = 0;
         HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, cfg.fn, threads, lds));
         HIPCHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, I->device));
@@ -1468,7 +1503,7 @@ int launch_draw(const csa_instance *I, int32_t k, uint64_t seed, uint64_t panel_
     void *args[] = {&A};
     HIPCHK(hipLaunchKernel(cfg.fn, dim3((unsigned)std::max<uint64_t>(1, grid)), dim3(threads), args, lds, stream));
     HIPCHK(hipGetLastError());
-    if (cfg.lane && !d_picks_ext) {  // pick lists -> packed panels (+ hashes)
+    if (cfg.picks() && !d_picks_ext) {  // pick lists -> packed panels (+ hashes)
         if ((rc = launch_pack(A.picks16, n_panels, k, I->W, d_panels, d_hashes, stream))) return rc;
         HIPCHK(hipEventRecord(M->picks_done, stream));
         M->picks_pending = true;
@@ -1785,7 +1820,7 @@ int32_t csa_picks_stride(int32_t k) { return (k + 7) & ~7; }
 int csa_draw_picks_supported(const csa_instance *I, int32_t k) {
     if (!I || check_k(I, k)) return 0;
     DrawConfig cfg;
-    return pick_draw_config(I, false, cfg) == CSA_OK && cfg.lane ? 1 : 0;
+    return pick_draw_config(I, false, cfg) == CSA_OK && cfg.picks() ? 1 : 0;
 }
 
 int csa_draw_picks_async(const csa_instance *I, int32_t k, uint64_t seed, uint64_t panel_begin, uint64_t n_panels,
@@ -1825,6 +1860,8 @@ int csa_draw_kernel_name(const csa_instance *I, int32_t k, char *buf, uint64_t l
     if (cfg.lane)
         snprintf(buf, (size_t)len, "draw_lane_kernel<%d, %d, %d>", cfg.FPL, cfg.WPL,
                  (cfg.WPL / 2 + CSA_LANE_SKDIV - 1) / CSA_LANE_SKDIV);
+    else if (cfg.wide)
+        snprintf(buf, (size_t)len, "draw_wide_kernel<%d, %d, %d>", cfg.G, cfg.FPL, cfg.WPL);
     else
         snprintf(buf, (size_t)len, "draw_kernel<%d, %d, %d, false>", cfg.G, cfg.FPL, cfg.WPL);
     return CSA_OK;

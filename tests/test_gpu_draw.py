@@ -1,8 +1,9 @@
 """GPU parity of every draw-kernel layout against the C oracle (Philox verification mode).
 
-The batch path picks draw_lane_kernel (2 lanes per panel, pick lists packed by
-picks_pack_kernel) or draw_kernel (G = 16 / 64) from the instance shape;
-CSA_DRAW_KERNEL=lane|16|64 forces a layout the instance fits.  Each must give the
+The batch path picks draw_lane_kernel (2 lanes per panel) or draw_wide_kernel (8 lanes per
+panel, n up to 8192), both writing pick lists that picks_pack_kernel packs, or draw_kernel
+(G = 16 / 64) from the instance shape; CSA_DRAW_KERNEL=lane|wide|16|64 forces a layout the
+instance fits.  Each must give the
 oracle's panels and attempt counts bit-exactly, including the edge cases of
 legacy.py:124-200 (restarts, rejections, max = 0 features, max = 0 < min).
 """
@@ -20,7 +21,7 @@ pytestmark = pytest.mark.gpu
 
 @pytest.fixture
 def draw_group():
-    """Force a batch draw layout (CSA_DRAW_KERNEL = "lane" / "16" / "64")."""
+    """Force a batch draw layout (CSA_DRAW_KERNEL = "lane" / "wide" / "16" / "64")."""
     old = os.environ.get("CSA_DRAW_KERNEL")
 
     def set_layout(g):
@@ -41,10 +42,11 @@ def _sample(enc, k, S, seed, begin=0, max_attempts=0):
     return panels, attempts
 
 
-@pytest.mark.parametrize("group", ["lane", 16, 64])
+@pytest.mark.parametrize("group", ["lane", "wide", 16, 64])
 @pytest.mark.parametrize("name,k,S,seed", [("sf_e_tight_110", 110, 3000, 5), ("pathological_5", 5, 4000, 2),
                                            ("rejecty_6", 6, 20000, 8), ("example_small_20", 20, 20000, 1),
-                                           ("couples_panel_from_twenty_people_no_constraints_2", 2, 20000, 3)])
+                                           ("couples_panel_from_twenty_people_no_constraints_2", 2, 20000, 3),
+                                           ("synthetic8192_200", 200, 2000, 6)])
 def test_draw_layouts_match_oracle(gpu_available, draw_group, group, name, k, S, seed):
     P = pkg()
     draw_group(group)
@@ -69,7 +71,7 @@ def _weird_instance():
     return cats, agents
 
 
-@pytest.mark.parametrize("group", ["lane", 16, 64])
+@pytest.mark.parametrize("group", ["lane", "wide", 16, 64])
 def test_zero_max_features_match_oracle(gpu_available, draw_group, group):
     """max = 0 features (dead, and max = 0 < min which routes to draw_kernel) vs the oracle."""
     P = pkg()
@@ -92,7 +94,7 @@ def test_zero_max_features_match_oracle(gpu_available, draw_group, group):
 
 
 @pytest.mark.parametrize("name,k,S,seed", [("sf_e_tight_110", 110, 3000, 5), ("example_small_20", 20, 5000, 3),
-                                           ("pathological_5", 5, 4000, 2)])
+                                           ("pathological_5", 5, 4000, 2), ("synthetic8192_200", 200, 3000, 4)])
 def test_pick_lists_match_oracle_pick_order(gpu_available, name, k, S, seed):
     """csa_draw_picks_async writes each accepted panel's picks in pick order (the order of
     people_selected, legacy.py:194); csa_picks_pack_async packs them (+ hashes) bit-exactly."""
