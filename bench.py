@@ -64,6 +64,9 @@ def parse():
                     help="serialise every stage on one stream (default: draws on their own stream, "
                          "--bufs - 1 steps ahead of the counting)")
     ap.add_argument("--bufs", type=int, default=3, help="panel buffers of the draw/count pipeline")
+    ap.add_argument("--pack-on", default="draw", choices=("draw", "count"),
+                    help="stream of picks_pack_kernel: after the draw on the draw stream, or first on the "
+                         "counting stream (one pick-list buffer per panel buffer)")
     ap.add_argument("--iso-steps", type=int, default=2,
                     help="serial steps after the timed region that measure each kernel alone (not in `value`)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -270,6 +273,8 @@ def main():
     draw_stream = torch.cuda.Stream(dev) if overlap else stream
     pbufs = [pipe.panels] + [torch.empty_like(pipe.panels) for _ in range(nb - 1)]
     hbufs = [pipe.hashes] + [torch.empty_like(pipe.hashes) for _ in range(nb - 1)]
+    pack_on_count = split and args.pack_on == "count"
+    kbufs = ([pipe.picks] + [torch.empty_like(pipe.picks) for _ in range(nb - 1)]) if pack_on_count else None
     drawn = [torch.cuda.Event() for _ in range(nb)]    # draw + pack of the buffer finished (draw stream)
     counted = [torch.cuda.Event() for _ in range(nb)]  # counting of the buffer finished (counting stream)
     stages = ["draw", "pack", "xt_count", "pairs", "unique", "exchange"]
@@ -287,6 +292,8 @@ def main():
         ds = stream if mode["serial"] else draw_stream
         ds.wait_event(counted[b])                 # step j - nb is done reading this buffer
         pipe.panels, pipe.hashes = pbufs[b], hbufs[b]
+        if pack_on_count:
+            pipe.picks = kbufs[b]
         begin = (j * world + rank) * S            # global panel indices, distinct per step and rank
         e = [Ev(), Ev(), Ev()] if rec is not None else None
         if e:
@@ -295,7 +302,8 @@ def main():
             pipe.draw_picks(args.seed, begin, S, stream=ds)
             if e:
                 e[1].record(ds)
-            pipe.pack(S, stream=ds)
+            if not pack_on_count:
+                pipe.pack(S, stream=ds)
         else:
             pipe.draw(args.seed, begin, S, stream=ds)
             if e:
@@ -309,8 +317,15 @@ def main():
         b = j % nb
         stream.wait_event(drawn[b])
         pipe.panels, pipe.hashes = pbufs[b], hbufs[b]
-        e = [Ev() for _ in range(5)] if rec is not None else None
+        e = [Ev() for _ in range(6)] if rec is not None else None
         pipe.reset(status=False, pairs=False)
+        if e:
+            e[5].record(stream)
+        if pack_on_count:
+            pipe.picks = kbufs[b]
+            pipe.pack(S, stream=stream)
+            if e:
+                rec[j]["pack"] = (e[5], e[0])
         if e:
             e[0].record(stream)
         pipe.transpose_count(S)
@@ -383,6 +398,11 @@ def main():
     # counting kernels share the CUs with the next steps' draws there.  A short serial pass AFTER
     # the timed region (not part of `value`) measures every kernel alone on the device.
     stage_pipe = stage_times(log)
+    # the draw stream's busy fraction in the timed region: ~1 when the host never lets it starve
+    # (draws are enqueued `ahead` steps before the counting / exchange that may block the host)
+    draw_busy = sum(ev["draw"][0].elapsed_time(ev["draw"][1]) + (ev["pack"][0].elapsed_time(ev["pack"][1])
+                                                                  if not pack_on_count else 0.0)
+                    for ev in log.values()) / (elapsed * 1e3) if log else None
     iso = {}
     if overlap and args.iso_steps:
         torch.cuda.synchronize()
@@ -489,6 +509,7 @@ def main():
         "kernels": kernels,
         "kernel_timing": kernel_timing,
         "checks": checks,
+        "draw_stream_busy": draw_busy,
     }
     if want_pairs:
         result["xtx_mfma_util"] = kernels["pairs_mfma"]["mfma_util"]

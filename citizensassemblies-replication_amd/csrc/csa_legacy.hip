@@ -607,41 +607,47 @@ __device__ __forceinline__ uint64_t wave_transpose64(uint64_t x, int lane) {
     return x;
 }
 
+// blockIdx.y = column range: words [CW y, CW y + CW) of every panel, i.e. agents [64 CW y, ...) --
+// one range for n <= 64 kXtCols agents, two for n up to 16384 (the tile and the counts of a range
+// fit the LDS)
+constexpr int kXtCols = 128;
 __global__ __launch_bounds__(kXtThreads) void xt_count_kernel(const uint64_t *__restrict__ panels,
                                                               uint64_t S, int n, int W, int npad,
                                                               uint64_t *__restrict__ xt,
                                                               int64_t *__restrict__ counts) {
     extern __shared__ uint64_t smem[];
-    const int Wp = W | 1;
+    const int c0 = (int)blockIdx.y * kXtCols, CW = min(kXtCols, W - c0);  // this block's word range
+    const int Wp = CW | 1;
+    const int p0 = 64 * c0, np = min(n - p0, 64 * CW);                   // its agents
     uint64_t *tile = smem;                                   // 64 x Wp
-    uint32_t *cnt = reinterpret_cast<uint32_t *>(smem + 64 * Wp);  // n
+    uint32_t *cnt = reinterpret_cast<uint32_t *>(smem + 64 * Wp);  // np
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nwv = blockDim.x >> 6;
-    for (int p = threadIdx.x; p < n; p += blockDim.x) cnt[p] = 0;
+    for (int p = threadIdx.x; p < np; p += blockDim.x) cnt[p] = 0;
     const uint64_t nblk = (S + 63) / 64;
     const uint64_t b0 = (uint64_t)blockIdx.x * kXtBlocksPerGroup;
     const uint64_t b1 = min(nblk, b0 + kXtBlocksPerGroup);
-    const int ncol = npad / 64;
+    const int ncol = min(npad / 64 - c0, kXtCols);  // transposed columns (padding included)
     for (uint64_t b = b0; b < b1; ++b) {
         __syncthreads();
         const uint64_t row0 = b * 64;
         const int rows = (int)min<uint64_t>(64, S - row0);
-        const uint64_t *src = panels + row0 * (uint64_t)W;
-        for (int t = threadIdx.x; t < 64 * W; t += blockDim.x) {
-            const int r = t / W, c = t - r * W;
-            tile[r * Wp + c] = r < rows ? src[t] : 0ull;
+        const uint64_t *src = panels + row0 * (uint64_t)W + c0;
+        for (int t = threadIdx.x; t < 64 * CW; t += blockDim.x) {
+            const int r = t / CW, c = t - r * CW;
+            tile[r * Wp + c] = r < rows ? src[(uint64_t)r * W + c] : 0ull;
         }
         __syncthreads();
         for (int w = wv; w < ncol; w += nwv) {
-            uint64_t x = w < W ? tile[lane * Wp + w] : 0ull;
+            uint64_t x = w < CW ? tile[lane * Wp + w] : 0ull;
             x = wave_transpose64(x, lane);
             const int p = 64 * w + lane;
-            if (xt) xt[b * (uint64_t)npad + p] = x;
-            if (p < n) cnt[p] += (uint32_t)__popcll(x);
+            if (xt) xt[b * (uint64_t)npad + p0 + p] = x;
+            if (p < np) cnt[p] += (uint32_t)__popcll(x);
         }
     }
     __syncthreads();
-    for (int p = threadIdx.x; p < n; p += blockDim.x)
-        if (cnt[p]) atomicAdd(reinterpret_cast<unsigned long long *>(counts + p), (unsigned long long)cnt[p]);
+    for (int p = threadIdx.x; p < np; p += blockDim.x)
+        if (cnt[p]) atomicAdd(reinterpret_cast<unsigned long long *>(counts + p0 + p), (unsigned long long)cnt[p]);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1873,12 +1879,13 @@ int csa_transpose_count_async(const uint64_t *d_panels, uint64_t n_panels, int32
                               int64_t *d_counts, void *stream) {
     if (n <= 0 || !d_panels || !d_counts) return fail(CSA_E_INVALID, "transpose: bad arguments");
     if (n_panels == 0) return CSA_OK;
-    const int W = (n + 63) / 64, Wp = W | 1;
-    const size_t lds = (size_t)64 * Wp * 8 + (size_t)n * 4;
+    const int W = (n + 63) / 64, CW = std::min(W, kXtCols), Wp = CW | 1;
+    const size_t lds = (size_t)64 * Wp * 8 + (size_t)std::min(n, 64 * CW) * 4;
     if (lds > 160 * 1024) return fail(CSA_E_UNSUPPORTED, "transpose needs %zu B of LDS", lds);
     const uint64_t nblk = (n_panels + 63) / 64;
     const unsigned grid = (unsigned)((nblk + kXtBlocksPerGroup - 1) / kXtBlocksPerGroup);
-    hipLaunchKernelGGL(xt_count_kernel, dim3(grid), dim3(kXtThreads), lds, (hipStream_t)stream, d_panels,
+    const unsigned ranges = (unsigned)((W + kXtCols - 1) / kXtCols);
+    hipLaunchKernelGGL(xt_count_kernel, dim3(grid, ranges), dim3(kXtThreads), lds, (hipStream_t)stream, d_panels,
                        n_panels, n, W, csa_xt_pad(n), d_xt, d_counts);
     HIPCHK(hipGetLastError());
     return CSA_OK;

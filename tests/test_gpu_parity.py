@@ -13,7 +13,8 @@ import pytest
 
 from conftest import PHILOX_CASES, golden, inst_paths, pkg
 from oracle import coracle
-from oracle.legacy_oracle import read_instance as oracle_read, draw_attempt, PhiloxRng, FAIL, NoCandidateError
+from oracle.legacy_oracle import read_instance as oracle_read, draw_attempt, PhiloxRng, FAIL, NoCandidateError, \
+    OracleInstance
 
 pytestmark = pytest.mark.gpu
 
@@ -446,3 +447,34 @@ def test_legacy_probabilities_distributed_gloo(gpu_available, tmp_path, name, k,
     assert np.array_equal(np.load(tmp_path / "upper.npy"), hist.upper())
     assert int(np.load(tmp_path / "unique.npy")[0]) == len(found)
     assert np.load(tmp_path / "found.npy").tolist() == [list(p) for p in sorted(found)]
+
+
+def test_n16384_boundary(gpu_available):
+    """The largest pool the header admits (n = 16384, W = 256): draw_kernel<16> for the draw,
+    xt_count_kernel over two column ranges, 64 x 64 triangle blocks of X^T X.  Panels, attempts,
+    counts and the distinct count vs the C oracle; pair counts vs a plain PyTorch fp32 X^T X."""
+    import torch
+    P = pkg()
+    A = pkg("analysis")
+    rng = np.random.default_rng(16384)
+    n, k, S = 16384, 300, 400
+    shares = {"a": [0.4, 0.3, 0.2, 0.1], "b": [0.5, 0.3, 0.2]}
+    cats = {c: {"%s%d" % (c, j): {"min": int(0.9 * k * p), "max": int(np.ceil(1.1 * k * p)) + 1}
+                for j, p in enumerate(ps)} for c, ps in shares.items()}
+    agents = {i: {c: "%s%d" % (c, rng.choice(len(ps), p=ps)) for c, ps in shares.items()} for i in range(n)}
+    enc = P.encode(cats, agents)
+    raw = A.legacy_sample_raw(enc, k, S, 21, want_pairs=True, want_panels=True, want_attempts=True)
+    feats = [(c, f) for c in cats for f in cats[c]]
+    o = OracleInstance(k=k, cat_names=list(cats), feat_names=feats,
+                       fmin=[cats[c][f]["min"] for c, f in feats], fmax=[cats[c][f]["max"] for c, f in feats],
+                       fcat=[list(cats).index(c) for c, f in feats],
+                       person_feat=[[feats.index((c, agents[i][c])) for c in cats] for i in range(n)])
+    rc, opanels, oatt, _ = coracle.draw(o, k, 21, 0, S)
+    assert rc == 0
+    assert np.array_equal(raw.panels, opanels)
+    assert np.array_equal(raw.attempts, oatt)
+    assert np.array_equal(raw.counts, coracle.counts(opanels, n))
+    assert raw.unique == coracle.unique(opanels, n)
+    X = torch.from_numpy(np.unpackbits(opanels.view(np.uint8), axis=1, bitorder="little")[:, :n]).cuda().float()
+    ref = (X.T @ X).to(torch.int64).cpu().numpy()
+    assert np.array_equal(np.triu(raw.pairs), np.triu(ref))

@@ -6,7 +6,7 @@ ROOT=${GRAFT_REPO_ROOT:-$(pwd)}; OUT=$ROOT/gpurun_out; mkdir -p "$OUT"; cd "$ROO
 TAG=${1:-cf}; shift || true
 CFGS=${*:-sf_e_110 example_large_200 synthetic8192 example_small_20 couples}
 for c in $CFGS; do
-  timeout -k 10 300 python bench.py --config $c --steps 3 --warmup 1 --no-cpu-baseline > "$OUT/bench_${TAG}_$c.json" 2> "$OUT/bench_${TAG}_$c.err"
+  timeout -k 10 300 python bench.py --config $c --steps 20 --warmup 2 --no-cpu-baseline --no-api > "$OUT/bench_${TAG}_$c.json" 2> "$OUT/bench_${TAG}_$c.err"
   rc=$?; echo "[bench $c] rc=$rc"
   [ $rc -eq 0 ] || { tail -5 "$OUT/bench_${TAG}_$c.err"; exit $rc; }
   python3 -c "
