@@ -587,7 +587,7 @@ __global__ __launch_bounds__(256) void panel_hash_kernel(const uint64_t *__restr
 // Bit transpose + per-person counts
 // ------------------------------------------------------------------------------------------
 constexpr int kXtThreads = 256;
-constexpr int kXtBlocksPerGroup = 16;  // 1024 panels per workgroup
+constexpr int kXtBlocksPerGroup = 16;  // at most 1024 panels per workgroup
 
 // 64x64 bit-matrix transpose across a wavefront: lane i holds row i (bit j = column j);
 // afterwards lane j holds column j (bit i = row i).
@@ -614,7 +614,7 @@ constexpr int kXtCols = 128;
 __global__ __launch_bounds__(kXtThreads) void xt_count_kernel(const uint64_t *__restrict__ panels,
                                                               uint64_t S, int n, int W, int npad,
                                                               uint64_t *__restrict__ xt,
-                                                              int64_t *__restrict__ counts) {
+                                                              int64_t *__restrict__ counts, int bpg) {
     extern __shared__ uint64_t smem[];
     const int c0 = (int)blockIdx.y * kXtCols, CW = min(kXtCols, W - c0);  // this block's word range
     const int Wp = CW | 1;
@@ -624,8 +624,8 @@ __global__ __launch_bounds__(kXtThreads) void xt_count_kernel(const uint64_t *__
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nwv = blockDim.x >> 6;
     for (int p = threadIdx.x; p < np; p += blockDim.x) cnt[p] = 0;
     const uint64_t nblk = (S + 63) / 64;
-    const uint64_t b0 = (uint64_t)blockIdx.x * kXtBlocksPerGroup;
-    const uint64_t b1 = min(nblk, b0 + kXtBlocksPerGroup);
+    const uint64_t b0 = (uint64_t)blockIdx.x * bpg;
+    const uint64_t b1 = min(nblk, b0 + (uint64_t)bpg);
     const int ncol = min(npad / 64 - c0, kXtCols);  // transposed columns (padding included)
     for (uint64_t b = b0; b < b1; ++b) {
         __syncthreads();
@@ -1411,11 +1411,20 @@ int lane_picks(csa_instance *I, uint64_t count, hipStream_t st, uint16_t **out) 
 int launch_pack(const uint16_t *d_picks, uint64_t n_panels, int k, int W, uint64_t *d_panels, uint64_t *d_hashes,
                 hipStream_t stream) {
     if (n_panels == 0) return CSA_OK;
-    const int wpb = W <= 16 ? 4 : W <= 64 ? 2 : 1;  // waves (64 panels each) per workgroup: <= 130 KB of LDS
-    const uint64_t blocks = (n_panels + 64 * wpb - 1) / (64 * wpb);
-    const size_t plds = (size_t)wpb * 64 * (2 * W + 1) * 4;
-    hipLaunchKernelGGL(picks_pack_kernel, dim3((unsigned)blocks), dim3(64 * wpb), plds, stream, d_picks, n_panels, k,
-                       W, d_panels, d_hashes);
+    // panels per wave: the largest power of two <= 64 whose tile (PK x (2W + 1) u32) stays near 8 KB
+    const size_t row = (size_t)(2 * W + 1) * 4;
+    const int pk = row * 64 <= 8704 ? 64 : row * 32 <= 8704 ? 32 : row * 16 <= 8704 ? 16 : row * 8 <= 8704 ? 8 : 4;
+    const int wpb = 4;
+    const uint64_t blocks = (n_panels + (uint64_t)pk * wpb - 1) / ((uint64_t)pk * wpb);
+    const size_t plds = (size_t)wpb * pk * row;
+    const void *fn = pk == 64   ? reinterpret_cast<const void *>(&picks_pack_kernel<64>)
+                     : pk == 32 ? reinterpret_cast<const void *>(&picks_pack_kernel<32>)
+                     : pk == 16 ? reinterpret_cast<const void *>(&picks_pack_kernel<16>)
+                     : pk == 8  ? reinterpret_cast<const void *>(&picks_pack_kernel<8>)
+                                : reinterpret_cast<const void *>(&picks_pack_kernel<4>);
+    if (plds > 160 * 1024) return fail(CSA_E_UNSUPPORTED, "picks_pack: W=%d too large", W);
+    void *args[] = {(void *)&d_picks, &n_panels, &k, &W, &d_panels, &d_hashes};
+    HIPCHK(hipLaunchKernel(fn, dim3((unsigned)blocks), dim3(64 * wpb), args, plds, stream));
     HIPCHK(hipGetLastError());
     return CSA_OK;
 }
@@ -1842,7 +1851,7 @@ int csa_picks_pack_async(const uint16_t *d_picks, uint64_t n_panels, int32_t k, 
     if (n <= 0 || n > 65536 || k < 0 || (k > 0 && !d_picks) || !d_panels)
         return fail(CSA_E_INVALID, "picks_pack: bad arguments");
     const int W = (n + 63) / 64;
-    if ((size_t)64 * (2 * W + 1) * 4 > 160 * 1024) return fail(CSA_E_UNSUPPORTED, "picks_pack: n=%d too large", n);
+    if ((size_t)4 * 4 * (2 * W + 1) * 4 > 160 * 1024) return fail(CSA_E_UNSUPPORTED, "picks_pack: n=%d too large", n);
     return launch_pack(d_picks, n_panels, k, W, d_panels, d_hashes, (hipStream_t)stream);
 }
 
@@ -1883,10 +1892,20 @@ int csa_transpose_count_async(const uint64_t *d_panels, uint64_t n_panels, int32
     const size_t lds = (size_t)64 * Wp * 8 + (size_t)std::min(n, 64 * CW) * 4;
     if (lds > 160 * 1024) return fail(CSA_E_UNSUPPORTED, "transpose needs %zu B of LDS", lds);
     const uint64_t nblk = (n_panels + 63) / 64;
-    const unsigned grid = (unsigned)((nblk + kXtBlocksPerGroup - 1) / kXtBlocksPerGroup);
     const unsigned ranges = (unsigned)((W + kXtCols - 1) / kXtCols);
+    // 64-panel blocks per workgroup: up to kXtBlocksPerGroup (fewer count flushes), but enough
+    // workgroups for two per CU (n = 8192, 10^5 panels: 4 blocks per workgroup, not 16)
+    static int cus = 0;
+    if (!cus) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+            cus = 256;
+    }
+    const uint64_t bpg = std::max<uint64_t>(1, std::min<uint64_t>(kXtBlocksPerGroup, nblk * ranges / (2 * (uint64_t)cus)));
+    const unsigned grid = (unsigned)((nblk + bpg - 1) / bpg);
     hipLaunchKernelGGL(xt_count_kernel, dim3(grid, ranges), dim3(kXtThreads), lds, (hipStream_t)stream, d_panels,
-                       n_panels, n, W, csa_xt_pad(n), d_xt, d_counts);
+                       n_panels, n, W, csa_xt_pad(n), d_xt, d_counts, (int)bpg);
     HIPCHK(hipGetLastError());
     return CSA_OK;
 }
