@@ -14,8 +14,9 @@ import ctypes
 import numpy as np
 
 from . import _native as N
+from . import legacy as _legacy
 from .instance import encode_cached, unpack_panel
-from .legacy import STREAM
+from .legacy import STREAM, mt_draw
 
 
 _ROW_CACHE = {}      # id(enc) -> (enc, {panel: packed row or None}); XMIN's portfolio grows by one per call
@@ -70,10 +71,20 @@ def first_panel_not_in(enc, k, seed, panel_begin, n_panels, packed_portfolio, ch
     return (idx.value, panel) if idx.value >= 0 else (-1, None)
 
 
-def _get_panel_not_in_portfolio_if_possible(categories, agents, k, portfolio, chunk=256):
-    """xmin.py:464-474 (same arguments, result and stream consumption)."""
+def _get_panel_not_in_portfolio_if_possible(categories, agents, k, portfolio, chunk=256, rng=None):
+    """xmin.py:464-474 (same arguments, result and stream consumption).  In MT mode (rng="mt" /
+    legacy.RNG_MODE) the legacy_find calls draw one by one from the stdlib random stream, as the
+    reference does, and the membership test stays on the host."""
     enc = encode_cached(categories, agents)
     tries = len(agents) * 3
+    if (rng or _legacy.RNG_MODE) == "mt":
+        members = {frozenset(p) for p in portfolio}
+        for _ in range(tries):
+            picks, _, _ = mt_draw(enc, k, 1)
+            panel = frozenset(enc.agent_ids[int(p)] for p in picks[0] if p >= 0)
+            if panel not in members:
+                return panel
+        return None
     first = STREAM.panel
     j, words = first_panel_not_in(enc, k, STREAM.key, first, tries, pack_portfolio(enc, portfolio), chunk=chunk)
     STREAM.take_panels(j + 1 if j >= 0 else tries)

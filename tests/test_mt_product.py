@@ -139,3 +139,25 @@ def test_mt_no_address_lines_match_reference_format():
     assert lines[0] == "Using legacy algorithm." and len(sel) == 110
     assert all(ln.startswith("Category ") and " full - deleted " in ln for ln in lines[1:])
     assert len(people) == len(inst.agents) - 110 - sum(int(ln.split("deleted ")[1].split(",")[0]) for ln in lines[1:])
+
+
+def test_mt_xmin_caller_consumes_like_the_reference():
+    """XMIN's caller in MT mode: one legacy_find per try from the stdlib stream, the first panel not
+    in the portfolio; the stream position afterwards equals drawing the same number of panels."""
+    P = pkg()
+    L = pkg("legacy")
+    X = pkg("xmin")
+    inst = P.read_instance(*inst_paths("couples_panel_from_twenty_people_no_constraints_2"), 2)
+    enc = P.encode(inst.categories, inst.agents)
+    random.seed(9)
+    picks, _, _ = L.mt_draw(enc, 2, 6)
+    panels = [frozenset(int(p) for p in row) for row in picks]
+    portfolio = list(dict.fromkeys(panels[:5]))               # the first five draws are members
+    random.seed(9)
+    got = X._get_panel_not_in_portfolio_if_possible(inst.categories, inst.agents, 2, portfolio, rng="mt")
+    want = next(p for p in panels if p not in portfolio)
+    assert got == want
+    after = random.getstate()
+    random.seed(9)
+    L.mt_draw(enc, 2, panels.index(want) + 1)
+    assert random.getstate() == after
