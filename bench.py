@@ -5,11 +5,10 @@ synthetic-instance panels per GPU, entirely on the device:
 draw (with restarts; pick lists) -> pack (packed panels + 128-bit hashes) ->
 bit transpose + per-person counts -> pair counts X^T X (fp4 MFMA) -> exact
 distinct-panel count, plus (N > 1) the exchange (RCCL all_reduce of counts and
-packed pairs, all_to_all of every panel to its owner rank + exact owner dedupe +
-all_reduce).  The draws run on their own stream, enqueued --bufs - 1 steps ahead
-of the counting, so the draw stream never waits for the host (the exchange's
-size negotiation synchronises the host with the counting stream only);
---no-overlap serialises everything on one stream.
+packed pairs, equal-split all_to_alls of the local distinct panels to their
+owner ranks + exact owner dedupe + all_reduce; nothing in it waits on the host).
+The draws run on their own stream, enqueued --bufs - 1 steps ahead of the
+counting; --no-overlap serialises everything on one stream.
 
     python bench.py [--gpus N --steps K --warmup W] [--config sf_e_110] [--panels P]
 
@@ -262,10 +261,11 @@ def main():
     engine_id, engine_peak, engine_desc = PAIR_ENGINES[args.pair_engine]
     pipe = Dv.DevicePipeline(enc, k, S, want_pairs=want_pairs, want_unique=True, device=dev, stream=stream,
                              pair_engine=engine_id)
-    table = Dd.HashTable(S * world, dev) if world > 1 else None
     draw_name = pipe.draw_kernel_name()   # the kernel csa_draw_async launches (matches rocprofv3 names)
     split = pipe.split_draw
     W = enc.W
+    # distinct-panel exchange buffers (fixed-capacity owner segments: no host sync per step)
+    xchg = Dd.PanelExchange(S, W, world, dev) if world > 1 else None
 
     overlap = not args.no_overlap
     nb = max(args.bufs, 2) if overlap else 1
@@ -343,7 +343,8 @@ def main():
         if world > 1:
             with torch.cuda.stream(stream):   # collectives order on the current stream
                 last["unique"] = Dd.combine(pipe.counts, pipe.pairs, pipe.hashes[: 2 * S], pipe.panels[: S * W], W,
-                                            table=table, stream=stream, pair_bound=S * world, status=pipe.status)[2]
+                                            exchange=xchg, stream=stream, pair_bound=S * world,
+                                            status=pipe.status)[2]
         if e:
             e[4].record(stream)
             rec[j].update({"xt_count": (e[0], e[1]), "pairs": (e[1], e[2]), "unique": (e[2], e[3]),

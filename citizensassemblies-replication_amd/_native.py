@@ -64,7 +64,9 @@ SIGNATURES = {
     "csa_pair_counts_async": (ctypes.c_int, [_P, _U64, _I32, _P, _P]),
     "csa_unique_async": (ctypes.c_int, [_P, _P, _U64, _I32, _P, _U64, _P, _P, _P]),
     "csa_pair_histogram_async": (ctypes.c_int, [_P, _I32, _P, _U64, _P, _P]),
-    "csa_hash_buckets_async": (ctypes.c_int, [_P, _P, _U64, _I32, _U32, _P, _P, _P, _P, _P]),
+    "csa_unique_segments_async": (ctypes.c_int, [_P, _P, _U32, _U64, _P, _I32, _P, _U64, _P, _P, _P]),
+    "csa_exchange_scratch_bytes": (_U64, [_U64]),
+    "csa_exchange_pack_async": (ctypes.c_int, [_P, _P, _U64, _I32, _U32, _U64, _P, _U64, _P, _P, _P, _P, _P]),
     "csa_pairs_pack_async": (ctypes.c_int, [_P, _I32, _P, _P]),
     "csa_pairs_unpack_async": (ctypes.c_int, [_P, _I32, _P, _P]),
     "csa_status_decode": (ctypes.c_int, [_P]),

@@ -874,14 +874,23 @@ __global__ __launch_bounds__(256) void pair_reduce_kernel(const int32_t *__restr
 // ------------------------------------------------------------------------------------------
 // Distinct panels
 // ------------------------------------------------------------------------------------------
+// Segmented input (the owner side of the multi-GPU exchange): entry i is valid iff
+// i % seg_cap < seg_counts[i / seg_cap]; without seg_counts every entry is.
+__device__ __forceinline__ bool uq_valid(uint64_t i, uint32_t seg_cap, const uint64_t *seg_counts) {
+    if (!seg_counts) return true;
+    const uint32_t s = (uint32_t)i / seg_cap;
+    return (uint64_t)((uint32_t)i - s * seg_cap) < seg_counts[s];
+}
+
 // one thread per panel: open addressing on `panel index + 1`, keyed by the 128-bit hash, exact
 // bitmask comparison on a hash match (small batches; the XMIN portfolio table)
 __global__ void unique_kernel(const uint64_t *__restrict__ hashes, const uint64_t *__restrict__ panels,
                               uint64_t S, int W, unsigned long long *__restrict__ table,
-                              uint64_t mask, unsigned long long *__restrict__ unique) {
+                              uint64_t mask, unsigned long long *__restrict__ unique, uint32_t seg_cap,
+                              const uint64_t *__restrict__ seg_counts) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     bool inserted = false;
-    if (i < S) {
+    if (i < S && uq_valid(i, seg_cap, seg_counts)) {
         const uint64_t h1 = hashes[2 * i], h2 = hashes[2 * i + 1];
         uint64_t slot = (h1 ^ (h2 >> 29)) & mask;
         for (uint64_t probe = 0; probe <= mask; ++probe) {
@@ -917,13 +926,15 @@ __device__ __forceinline__ uint32_t uq_part(uint64_t h1, int pbits) { return (ui
 
 __global__ __launch_bounds__(kUqThreads) void uq_count_kernel(const uint64_t *__restrict__ hashes, uint64_t S,
                                                               uint64_t CH, int pbits, uint32_t nwg,
-                                                              uint32_t *__restrict__ hist) {
+                                                              uint32_t *__restrict__ hist, uint32_t seg_cap,
+                                                              const uint64_t *__restrict__ seg_counts) {
     __shared__ uint32_t h[kUqMaxParts];
     const uint32_t P = 1u << pbits;
     for (uint32_t p = threadIdx.x; p < P; p += blockDim.x) h[p] = 0;
     __syncthreads();
     const uint64_t b0 = (uint64_t)blockIdx.x * CH, b1 = min(S, b0 + CH);
-    for (uint64_t i = b0 + threadIdx.x; i < b1; i += blockDim.x) atomicAdd(&h[uq_part(hashes[2 * i], pbits)], 1u);
+    for (uint64_t i = b0 + threadIdx.x; i < b1; i += blockDim.x)
+        if (uq_valid(i, seg_cap, seg_counts)) atomicAdd(&h[uq_part(hashes[2 * i], pbits)], 1u);
     __syncthreads();
     for (uint32_t p = threadIdx.x; p < P; p += blockDim.x) hist[(uint64_t)p * nwg + blockIdx.x] = h[p];
 }
@@ -986,14 +997,15 @@ __global__ __launch_bounds__(kUqThreads) void uq_scatter_kernel(const uint64_t *
                                                                 uint64_t CH, int pbits, uint32_t nwg,
                                                                 const uint32_t *__restrict__ hist,
                                                                 const uint32_t *__restrict__ base,
-                                                                uint32_t *__restrict__ idx) {
+                                                                uint32_t *__restrict__ idx, uint32_t seg_cap,
+                                                                const uint64_t *__restrict__ seg_counts) {
     __shared__ uint32_t ctr[kUqMaxParts];
     const uint32_t P = 1u << pbits;
     for (uint32_t p = threadIdx.x; p < P; p += blockDim.x) ctr[p] = base[p] + hist[(uint64_t)p * nwg + blockIdx.x];
     __syncthreads();
     const uint64_t b0 = (uint64_t)blockIdx.x * CH, b1 = min(S, b0 + CH);
     for (uint64_t i = b0 + threadIdx.x; i < b1; i += blockDim.x)
-        idx[atomicAdd(&ctr[uq_part(hashes[2 * i], pbits)], 1u)] = (uint32_t)i;
+        if (uq_valid(i, seg_cap, seg_counts)) idx[atomicAdd(&ctr[uq_part(hashes[2 * i], pbits)], 1u)] = (uint32_t)i;
 }
 
 // one workgroup per partition: exact dedupe in an LDS table of panel indices
@@ -1002,9 +1014,11 @@ __global__ __launch_bounds__(kUqThreads) void uq_dedupe_kernel(const uint64_t *_
                                                                const uint32_t *__restrict__ idx,
                                                                const uint32_t *__restrict__ base,
                                                                unsigned long long *__restrict__ unique,
-                                                               uint32_t *__restrict__ status) {
+                                                               uint32_t *__restrict__ status,
+                                                               uint32_t *__restrict__ rep,
+                                                               unsigned long long *__restrict__ rep_count) {
     __shared__ uint32_t T[kUqTable];
-    __shared__ uint32_t cnt;
+    __shared__ uint32_t cnt, rbase, rpos;
     for (int t = threadIdx.x; t < kUqTable; t += blockDim.x) T[t] = 0;
     if (threadIdx.x == 0) cnt = 0;
     __syncthreads();
@@ -1036,7 +1050,16 @@ __global__ __launch_bounds__(kUqThreads) void uq_dedupe_kernel(const uint64_t *_
     }
     atomicAdd(&cnt, mine);
     __syncthreads();
-    if (threadIdx.x == 0 && cnt) atomicAdd(unique, (unsigned long long)cnt);
+    if (threadIdx.x == 0 && cnt && unique) atomicAdd(unique, (unsigned long long)cnt);
+    if (rep) {  // the partition's distinct panels (its table entries) -> rep[], one global atomic per workgroup
+        if (threadIdx.x == 0) {
+            rbase = cnt ? (uint32_t)atomicAdd(rep_count, (unsigned long long)cnt) : 0u;
+            rpos = 0;
+        }
+        __syncthreads();
+        for (int t = threadIdx.x; t < kUqTable; t += blockDim.x)
+            if (T[t]) rep[rbase + atomicAdd(&rpos, 1u)] = T[t] - 1u;
+    }
 }
 
 // Portfolio membership of drawn panels (xmin.py:468-469: `panel not in portfolio`): probe the
@@ -1082,46 +1105,64 @@ __global__ __launch_bounds__(256) void pair_histogram_kernel(const int64_t *__re
     }
 }
 
-// Owner buckets of 128-bit panel hashes for the multi-GPU distinct-panel exchange
-// (owner = h1 % world): pass 1 counts per owner, pass 2 scatters each hash
-// to its owner's range (order inside a bucket is irrelevant to the distinct count).
+// Multi-GPU distinct-panel exchange, send side (owner = h1 % world): the
+// local distinct panels (rep[0 .. *rep_count), from the partitioned dedupe) go into fixed-capacity
+// segments of send_hashes / send_panels, one segment per owner rank, so the all_to_all has equal
+// splits and the host never reads a size.  send_counts[w] (zeroed by the caller) = entries reserved in
+// segment w; a segment past its capacity raises CSA_E_UNSUPPORTED (kExchangeOverflow) in the status
+// block.  Per workgroup: LDS histogram per owner, one global atomic per (workgroup, owner) to reserve
+// ranges, the hashes, then the panel rows copied cooperatively (W contiguous words per row).
 constexpr int kMaxWorld = 1024;
-__global__ __launch_bounds__(256) void hash_owner_count_kernel(const uint64_t *__restrict__ hashes, uint64_t n,
-                                                               uint32_t world, unsigned long long *__restrict__ counts) {
-    __shared__ uint32_t c[kMaxWorld];
-    for (uint32_t w = threadIdx.x; w < world; w += blockDim.x) c[w] = 0;
+constexpr int kXbThreads = 256;
+constexpr uint64_t kExchangeOverflow = 0xFFFFFFFFFFFFFFFEull;  // status "panel" of a full segment
+__global__ __launch_bounds__(kXbThreads) void exchange_bucket_kernel(
+    const uint64_t *__restrict__ hashes, const uint64_t *__restrict__ panels, int W, const uint32_t *__restrict__ rep,
+    const unsigned long long *__restrict__ rep_count, uint32_t world, uint64_t capacity,
+    uint64_t *__restrict__ send_hashes, uint64_t *__restrict__ send_panels,
+    unsigned long long *__restrict__ send_counts, uint32_t *__restrict__ status) {
+    __shared__ uint32_t hist[kMaxWorld];
+    __shared__ unsigned long long rbase[kMaxWorld];
+    __shared__ uint32_t src_row[kXbThreads];
+    __shared__ uint64_t dst_row[kXbThreads];
+    const uint64_t m = *rep_count;
+    const uint64_t e0 = (uint64_t)blockIdx.x * kXbThreads;
+    if (e0 >= m) return;  // whole workgroup
+    for (uint32_t w = threadIdx.x; w < world; w += blockDim.x) hist[w] = 0;
     __syncthreads();
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
-        atomicAdd(&c[hashes[2 * i] % world], 1u);
+    const uint64_t e = e0 + threadIdx.x;
+    const bool valid = e < m;
+    uint32_t i = 0, owner = 0, local = 0;
+    uint64_t h1 = 0, h2 = 0;
+    if (valid) {
+        i = rep[e];
+        h1 = hashes[2 * (uint64_t)i];
+        h2 = hashes[2 * (uint64_t)i + 1];
+        owner = (uint32_t)(h1 % world);
+        local = atomicAdd(&hist[owner], 1u);
+    }
     __syncthreads();
     for (uint32_t w = threadIdx.x; w < world; w += blockDim.x)
-        if (c[w]) atomicAdd(counts + w, (unsigned long long)c[w]);
-}
-
-__global__ __launch_bounds__(256) void hash_owner_scatter_kernel(const uint64_t *__restrict__ hashes,
-                                                                 const uint64_t *__restrict__ panels, uint64_t n,
-                                                                 int W, uint32_t world,
-                                                                 unsigned long long *__restrict__ cursor,
-                                                                 uint64_t *__restrict__ out,
-                                                                 uint64_t *__restrict__ out_panels) {
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
-        const uint64_t h1 = hashes[2 * i], h2 = hashes[2 * i + 1];
-        const unsigned long long pos = atomicAdd(cursor + (h1 % world), 1ull);
-        out[2 * pos] = h1;
-        out[2 * pos + 1] = h2;
-        if (panels)  // the bitmask travels with its hash: the owner's dedupe compares bitmasks
-            for (int w = 0; w < W; ++w) out_panels[pos * W + w] = panels[i * W + w];
-    }
-}
-
-__global__ void exclusive_scan_small_kernel(const unsigned long long *__restrict__ counts, uint32_t world,
-                                            unsigned long long *__restrict__ cursor) {
-    if (threadIdx.x == 0 && blockIdx.x == 0) {
-        unsigned long long acc = 0;
-        for (uint32_t w = 0; w < world; ++w) {
-            cursor[w] = acc;
-            acc += counts[w];
+        rbase[w] = hist[w] ? atomicAdd(&send_counts[w], (unsigned long long)hist[w]) : 0ull;
+    __syncthreads();
+    uint64_t dst = ~0ull;
+    if (valid) {
+        const uint64_t pos = rbase[owner] + local;
+        if (pos < capacity) {
+            dst = (uint64_t)owner * capacity + pos;
+            send_hashes[2 * dst] = h1;
+            send_hashes[2 * dst + 1] = h2;
+        } else {
+            raise_status(status, CSA_E_UNSUPPORTED, kExchangeOverflow);
         }
+    }
+    src_row[threadIdx.x] = i;
+    dst_row[threadIdx.x] = dst;
+    __syncthreads();
+    const uint32_t rows = (uint32_t)min<uint64_t>(kXbThreads, m - e0);
+    for (uint32_t t = threadIdx.x; t < rows * (uint32_t)W; t += blockDim.x) {
+        const uint32_t r = t / (uint32_t)W, w = t - r * (uint32_t)W;
+        const uint64_t d = dst_row[r];
+        if (d != ~0ull) send_panels[d * W + w] = panels[(uint64_t)src_row[r] * W + w];
     }
 }
 
@@ -1569,6 +1610,71 @@ int scratch(csa_instance *I, int slot, size_t count, T **out) {
 
 }  // namespace
 
+namespace {
+// Partitioned distinct pass (no per-panel global atomics): hashes partitioned by their top bits
+// (counting pass -> scans -> scatter), then one workgroup per partition dedupes in an LDS table
+// (equal 128-bit hashes AND equal bitmasks).  It counts (unique) and/or lists one index per
+// distinct panel (rep); seg_counts restricts it to the valid entries of segmented input.
+struct UqPlan {
+    int pbits = 6;
+    uint64_t P = 64, CH = 4096, scratch_bytes = 0;
+    uint32_t nwg = 1;
+    bool fits = true;  // partitions average <= 2048 entries (an 8192-slot LDS table each)
+};
+
+void uq_plan(uint64_t n, UqPlan &q) {
+    q.pbits = 6;
+    while ((1ull << q.pbits) * 1024 < n && q.pbits < 13) ++q.pbits;
+    q.P = 1ull << q.pbits;
+    q.CH = std::max<uint64_t>(4096, ((n + 1023) / 1024 + 255) / 256 * 256);
+    q.nwg = (uint32_t)((n + q.CH - 1) / q.CH);
+    q.scratch_bytes = 4 * n + 4 * q.P * q.nwg + 4 * q.P + 4 * (q.P + 1);
+    q.fits = n < (1ull << 31) && n / q.P <= 2048;
+}
+
+int uq_partitioned(const uint64_t *d_hashes, const uint64_t *d_panels, uint64_t n, int W, const UqPlan &q,
+                   uint32_t *scratch, uint64_t *d_unique, uint32_t *d_status, uint32_t seg_cap,
+                   const uint64_t *seg_counts, uint32_t *rep, unsigned long long *rep_count, hipStream_t st) {
+    if (!q.fits) return fail(CSA_E_UNSUPPORTED, "distinct panels: %llu entries exceed the partitioned path",
+                             (unsigned long long)n);
+    uint32_t *idx = scratch, *hist = idx + n, *tot = hist + q.P * q.nwg, *pbase = tot + q.P;
+    hipLaunchKernelGGL(uq_count_kernel, dim3(q.nwg), dim3(kUqThreads), 0, st, d_hashes, n, q.CH, q.pbits, q.nwg, hist,
+                       seg_cap, seg_counts);
+    hipLaunchKernelGGL(uq_scan_part_kernel, dim3((unsigned)q.P), dim3(kUqThreads), 0, st, hist, q.nwg, tot);
+    hipLaunchKernelGGL(uq_scan_tot_kernel, dim3(1), dim3(1024), 0, st, tot, (uint32_t)q.P, pbase);
+    hipLaunchKernelGGL(uq_scatter_kernel, dim3(q.nwg), dim3(kUqThreads), 0, st, d_hashes, n, q.CH, q.pbits, q.nwg,
+                       hist, pbase, idx, seg_cap, seg_counts);
+    hipLaunchKernelGGL(uq_dedupe_kernel, dim3((unsigned)q.P), dim3(kUqThreads), 0, st, d_hashes, d_panels, W, idx,
+                       pbase, reinterpret_cast<unsigned long long *>(d_unique), d_status, rep, rep_count);
+    HIPCHK(hipGetLastError());
+    return CSA_OK;
+}
+
+// csa_unique_async / csa_unique_segments_async: the partitioned path for large batches with a status
+// block (its LDS tables report an overflow there), else one global open-addressing table
+int unique_impl(const uint64_t *d_hashes, const uint64_t *d_panels, uint64_t n_panels, int32_t W, uint64_t *d_table,
+                uint64_t table_slots, uint64_t *d_unique, uint32_t *d_status, uint32_t seg_cap,
+                const uint64_t *seg_counts, hipStream_t st) {
+    if (!d_hashes || !d_panels || !d_table || !d_unique || W <= 0) return fail(CSA_E_INVALID, "unique: bad arguments");
+    if (table_slots < 2 * n_panels || (table_slots & (table_slots - 1)))
+        return fail(CSA_E_INVALID, "unique: table_slots must be a power of two >= 2*n_panels");
+    if (n_panels == 0) return CSA_OK;
+    UqPlan q;
+    uq_plan(n_panels, q);
+    const char *ue = getenv("CSA_UNIQUE_PART");
+    if (d_status && n_panels >= 65536 && q.fits && q.scratch_bytes <= table_slots * 8 && !(ue && atoi(ue) == 0))
+        return uq_partitioned(d_hashes, d_panels, n_panels, W, q, reinterpret_cast<uint32_t *>(d_table), d_unique,
+                              d_status, seg_cap, seg_counts, nullptr, nullptr, st);
+    HIPCHK(hipMemsetAsync(d_table, 0, table_slots * 8, st));
+    const unsigned grid = (unsigned)((n_panels + 255) / 256);
+    hipLaunchKernelGGL(unique_kernel, dim3(grid), dim3(256), 0, st, d_hashes, d_panels, n_panels, W,
+                       reinterpret_cast<unsigned long long *>(d_table), table_slots - 1,
+                       reinterpret_cast<unsigned long long *>(d_unique), seg_cap, seg_counts);
+    HIPCHK(hipGetLastError());
+    return CSA_OK;
+}
+}  // namespace
+
 extern "C" {
 
 int csa_version(void) { return 1; }
@@ -1763,33 +1869,6 @@ int csa_pair_histogram_async(const int64_t *d_pairs, int32_t n, uint64_t *d_hist
     return CSA_OK;
 }
 
-int csa_hash_buckets_async(const uint64_t *d_hashes, const uint64_t *d_panels, uint64_t n_hashes, int32_t W,
-                           uint32_t world, uint64_t *d_out, uint64_t *d_out_panels, uint64_t *d_counts,
-                           uint64_t *d_cursor, void *stream) {
-    if (!d_hashes || !d_out || !d_counts || !d_cursor || world == 0 || world > (uint32_t)kMaxWorld ||
-        (d_panels && (!d_out_panels || W <= 0)))
-        return fail(CSA_E_INVALID, "hash buckets: bad arguments");
-    hipStream_t st = (hipStream_t)stream;
-    HIPCHK(hipMemsetAsync(d_counts, 0, (size_t)world * 8, st));
-    if (n_hashes) {
-        const unsigned grid = (unsigned)std::min<uint64_t>((n_hashes + 255) / 256, 2048);
-        hipLaunchKernelGGL(hash_owner_count_kernel, dim3(grid), dim3(256), 0, st, d_hashes, n_hashes, world,
-                           reinterpret_cast<unsigned long long *>(d_counts));
-        HIPCHK(hipGetLastError());
-    }
-    hipLaunchKernelGGL(exclusive_scan_small_kernel, dim3(1), dim3(64), 0, st,
-                       reinterpret_cast<const unsigned long long *>(d_counts), world,
-                       reinterpret_cast<unsigned long long *>(d_cursor));
-    HIPCHK(hipGetLastError());
-    if (n_hashes) {
-        const unsigned grid = (unsigned)std::min<uint64_t>((n_hashes + 255) / 256, 2048);
-        hipLaunchKernelGGL(hash_owner_scatter_kernel, dim3(grid), dim3(256), 0, st, d_hashes, d_panels, n_hashes, W,
-                           world, reinterpret_cast<unsigned long long *>(d_cursor), d_out, d_out_panels);
-        HIPCHK(hipGetLastError());
-    }
-    return CSA_OK;
-}
-
 int csa_pairs_pack_async(const int64_t *d_pairs, int32_t n, int32_t *d_packed, void *stream) {
     if (n <= 0 || !d_pairs || !d_packed) return fail(CSA_E_INVALID, "pairs pack: bad arguments");
     hipLaunchKernelGGL(pairs_pack_kernel, dim3((unsigned)n), dim3(256), 0, (hipStream_t)stream, d_pairs, n, d_packed);
@@ -1817,6 +1896,12 @@ int csa_status_decode(const uint32_t *h) {
         case CSA_E_ATTEMPT_LIMIT:
             return fail(CSA_E_ATTEMPT_LIMIT, "panel %llu: attempt limit reached without an accepted panel",
                         (unsigned long long)panel);
+        case CSA_E_UNSUPPORTED:
+            if (panel == kExchangeOverflow)
+                return fail(CSA_E_UNSUPPORTED, "distinct-panel exchange: an owner segment exceeded its capacity");
+            if (panel == 0xFFFFFFFFFFFFFFFFull)
+                return fail(CSA_E_UNSUPPORTED, "distinct panels: a partition exceeded its LDS table");
+            return fail(CSA_E_UNSUPPORTED, "device status %u at panel %llu", h[0], (unsigned long long)panel);
         default:
             return fail((int)h[0], "device status %u at panel %llu", h[0], (unsigned long long)panel);
     }
@@ -1983,44 +2068,52 @@ int csa_pair_counts_async(const uint64_t *d_xt, uint64_t n_blocks, int32_t n, in
 
 int csa_unique_async(const uint64_t *d_hashes, const uint64_t *d_panels, uint64_t n_panels, int32_t W,
                      uint64_t *d_table, uint64_t table_slots, uint64_t *d_unique, uint32_t *d_status, void *stream) {
-    if (!d_hashes || !d_panels || !d_table || !d_unique || W <= 0) return fail(CSA_E_INVALID, "unique: bad arguments");
-    if (table_slots < 2 * n_panels || (table_slots & (table_slots - 1)))
-        return fail(CSA_E_INVALID, "unique: table_slots must be a power of two >= 2*n_panels");
-    if (n_panels == 0) return CSA_OK;
+    return unique_impl(d_hashes, d_panels, n_panels, W, d_table, table_slots, d_unique, d_status, 0, nullptr,
+                       (hipStream_t)stream);
+}
+
+int csa_unique_segments_async(const uint64_t *d_hashes, const uint64_t *d_panels, uint32_t n_segments,
+                              uint64_t capacity, const uint64_t *d_seg_counts, int32_t W, uint64_t *d_table,
+                              uint64_t table_slots, uint64_t *d_unique, uint32_t *d_status, void *stream) {
+    if (!d_seg_counts || capacity == 0 || capacity > 0xFFFFFFFFull)
+        return fail(CSA_E_INVALID, "unique segments: bad arguments");
+    return unique_impl(d_hashes, d_panels, (uint64_t)n_segments * capacity, W, d_table, table_slots, d_unique,
+                       d_status, (uint32_t)capacity, d_seg_counts, (hipStream_t)stream);
+}
+
+uint64_t csa_exchange_scratch_bytes(uint64_t n_panels) {
+    UqPlan q;
+    uq_plan(std::max<uint64_t>(n_panels, 1), q);
+    return 8 + 4 * std::max<uint64_t>(n_panels, 1) + q.scratch_bytes + 8;
+}
+
+int csa_exchange_pack_async(const uint64_t *d_hashes, const uint64_t *d_panels, uint64_t n_panels, int32_t W,
+                            uint32_t world, uint64_t capacity, void *d_scratch, uint64_t scratch_bytes,
+                            uint64_t *d_send_hashes, uint64_t *d_send_panels, uint64_t *d_send_counts,
+                            uint32_t *d_status, void *stream) {
+    if (!d_hashes || !d_panels || W <= 0 || world == 0 || world > (uint32_t)kMaxWorld || capacity == 0 ||
+        !d_scratch || !d_send_hashes || !d_send_panels || !d_send_counts || !d_status)
+        return fail(CSA_E_INVALID, "exchange pack: bad arguments");
+    if (n_panels >= (1ull << 31)) return fail(CSA_E_UNSUPPORTED, "exchange pack: n_panels >= 2^31");
+    if (scratch_bytes < csa_exchange_scratch_bytes(n_panels))
+        return fail(CSA_E_INVALID, "exchange pack: scratch_bytes < csa_exchange_scratch_bytes(n_panels)");
     const hipStream_t st = (hipStream_t)stream;
-    // partitioned path for large batches with bitmasks (the table memory holds its buffers)
-    int pbits = 6;
-    while ((1ull << pbits) * 1024 < n_panels && pbits < 13) ++pbits;
-    const uint64_t P = 1ull << pbits;
-    const char *ue = getenv("CSA_UNIQUE_PART");
-    // (its per-partition LDS tables report an overflow through d_status: without one, the
-    // single-table path, which cannot overflow, runs)
-    const bool part = d_status && n_panels >= 65536 && n_panels < (1ull << 31) && n_panels / P <= 2048 &&
-                      !(ue && atoi(ue) == 0);
-    if (part) {
-        const uint64_t CH = std::max<uint64_t>(4096, ((n_panels + 1023) / 1024 + 255) / 256 * 256);
-        const uint32_t nwg = (uint32_t)((n_panels + CH - 1) / CH);
-        const uint64_t need = 4 * n_panels + 4 * P * nwg + 4 * P + 4 * (P + 1);
-        if (need <= table_slots * 8) {
-            uint32_t *idx = reinterpret_cast<uint32_t *>(d_table);
-            uint32_t *hist = idx + n_panels, *tot = hist + P * nwg, *pbase = tot + P;
-            hipLaunchKernelGGL(uq_count_kernel, dim3(nwg), dim3(kUqThreads), 0, st, d_hashes, n_panels, CH, pbits,
-                               nwg, hist);
-            hipLaunchKernelGGL(uq_scan_part_kernel, dim3((unsigned)P), dim3(kUqThreads), 0, st, hist, nwg, tot);
-            hipLaunchKernelGGL(uq_scan_tot_kernel, dim3(1), dim3(1024), 0, st, tot, (uint32_t)P, pbase);
-            hipLaunchKernelGGL(uq_scatter_kernel, dim3(nwg), dim3(kUqThreads), 0, st, d_hashes, n_panels, CH, pbits,
-                               nwg, hist, pbase, idx);
-            hipLaunchKernelGGL(uq_dedupe_kernel, dim3((unsigned)P), dim3(kUqThreads), 0, st, d_hashes, d_panels, W,
-                               idx, pbase, reinterpret_cast<unsigned long long *>(d_unique), d_status);
-            HIPCHK(hipGetLastError());
-            return CSA_OK;
-        }
-    }
-    HIPCHK(hipMemsetAsync(d_table, 0, table_slots * 8, st));
-    const unsigned grid = (unsigned)((n_panels + 255) / 256);
-    hipLaunchKernelGGL(unique_kernel, dim3(grid), dim3(256), 0, st, d_hashes, d_panels, n_panels, W,
-                       reinterpret_cast<unsigned long long *>(d_table), table_slots - 1,
-                       reinterpret_cast<unsigned long long *>(d_unique));
+    unsigned long long *rep_count = reinterpret_cast<unsigned long long *>(d_scratch);
+    uint32_t *rep = reinterpret_cast<uint32_t *>(rep_count + 1);
+    uint32_t *part = rep + ((std::max<uint64_t>(n_panels, 1) + 1) & ~1ull);  // 8-byte aligned
+    HIPCHK(hipMemsetAsync(rep_count, 0, 8, st));
+    HIPCHK(hipMemsetAsync(d_send_counts, 0, (size_t)world * 8, st));
+    if (n_panels == 0) return CSA_OK;
+    // 1. the local distinct panels (exact: hash AND bitmask), their indices into rep[]
+    UqPlan q;
+    uq_plan(n_panels, q);
+    int rc = uq_partitioned(d_hashes, d_panels, n_panels, W, q, part, nullptr, d_status, 0, nullptr, rep, rep_count, st);
+    if (rc) return rc;
+    // 2. bucket them by owner into the fixed-capacity segments
+    const unsigned grid = (unsigned)((n_panels + kXbThreads - 1) / kXbThreads);
+    hipLaunchKernelGGL(exchange_bucket_kernel, dim3(grid), dim3(kXbThreads), 0, st, d_hashes, d_panels, W, rep,
+                       rep_count, world, capacity, d_send_hashes, d_send_panels,
+                       reinterpret_cast<unsigned long long *>(d_send_counts), d_status);
     HIPCHK(hipGetLastError());
     return CSA_OK;
 }

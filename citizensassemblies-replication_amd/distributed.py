@@ -6,25 +6,28 @@ index (Philox counter = (step, attempt, panel)), so the union of the shards is
 bit-identical to a single-GPU run for any world size; no data-path collective
 is needed for the draw itself.
 
-Exchange steps (the only collectives on the path):
+Exchange steps (the only collectives on the path), all
+stream-ordered -- the host never waits for the device:
   * per-person counts  all_reduce(SUM) int64[n]
   * pair counts        all_reduce(SUM) of the upper triangle packed to int32
                        (csa_pairs_pack/unpack_async; int64[n*n] if a count may
                        reach 2^31)
-  * distinct panels    every panel -- its 128-bit hash AND its W-word bitmask --
-                       goes to its OWNER rank (h1 % world; equal panels have
-                       equal hashes, so all copies of a panel meet at one owner)
-                       with all_to_all (buckets from csa_hash_buckets_async); the
-                       owner counts its distinct panels with csa_unique_async,
-                       which compares bitmasks on a hash match, so the count is
-                       exact (analysis.py:171,186: a set of sorted tuples); then
-                       all_reduce(SUM) of the owners' counts.
-The bucket sizes are negotiated with a small all_to_all whose result the host
-reads (the only host synchronisation of the exchange); bench.py enqueues the
-next steps' draws before it, so the draw stream never waits for it.
-On CPU (gloo, tests) the same exchange runs on host tensors: numpy bucketing by
-owner and an exact numpy dedupe of the bitmasks; ``panel_hashes`` mirrors the
-device hash for that path.
+  * distinct panels    each rank first reduces its panels to its exact LOCAL
+                       distinct set (hash AND bitmask), then sends every one --
+                       its 128-bit hash and W-word bitmask -- to its OWNER rank
+                       (h1 % world; equal panels have equal hashes, so all copies
+                       of a panel meet at one owner).  The segments per owner have
+                       a FIXED capacity (binomial bound on a uniform hash, see
+                       exchange_capacity), so the three all_to_alls (segment
+                       counts, hashes, bitmasks) have equal splits and need no
+                       host-side size negotiation (csa_exchange_pack_async).  The
+                       owner counts the distinct panels among the valid entries
+                       exactly (csa_unique_segments_async: bitmask comparison on a
+                       hash match; analysis.py:171,186 is a set of sorted tuples),
+                       then all_reduce(SUM).  A segment past its capacity is an
+                       error in the status block, never a wrong count.
+On CPU (gloo, tests) the same exchange runs on host tensors with numpy mirrors
+of the two kernels; ``panel_hashes`` mirrors the device hash for that path.
 """
 import ctypes
 import os
@@ -83,14 +86,45 @@ def panel_hashes(panels):
     return np.stack([h1, h2], axis=1)
 
 
-def owner_buckets(hashes, panels, world):
-    """Host mirror of csa_hash_buckets_async: (hashes, panels, counts) in owner-major order,
-    owner = h1 % world."""
+def exchange_capacity(n_local, world):
+    """Entries per owner segment for a rank with n_local panels: the distinct panels reaching one
+    owner are Binomial(m <= n_local, 1/world) under a uniform hash, so mean + 8 sd + 64 never
+    overflows in practice (P < 1e-15 per segment); never more than n_local."""
+    n_local, world = max(int(n_local), 1), int(world)
+    mean = -(-n_local // world)
+    return min(n_local, mean + 8 * int(mean ** 0.5 + 1) + 64)
+
+
+def local_distinct(hashes, panels):
+    """Host mirror of the first stage of csa_exchange_pack_async: the exact distinct rows (hash AND
+    bitmask) of uint64[m, 2] / uint64[m, W]."""
     h = np.asarray(hashes, np.uint64).reshape(-1, 2)
-    p = np.asarray(panels, np.uint64).reshape(len(h), -1)
-    owner = (h[:, 0] % np.uint64(world)).astype(np.int64)
-    order = np.argsort(owner, kind="stable")
-    return h[order], p[order], np.bincount(owner, minlength=world).astype(np.int64)
+    p = np.asarray(panels, np.uint64)
+    assert p.ndim == 2 and len(p) == len(h)
+    if len(h) == 0:
+        return h, p
+    u = np.unique(np.concatenate([h, p], axis=1), axis=0)
+    return np.ascontiguousarray(u[:, :2]), np.ascontiguousarray(u[:, 2:])
+
+
+def segment_buckets(hashes, panels, world, cap):
+    """Host mirror of csa_exchange_pack_async (panels uint64[m, W]): the local distinct panels in
+    fixed-capacity owner segments.  Returns (uint64[world, cap, 2], uint64[world, cap, W], int64[world] counts)."""
+    h, p = local_distinct(hashes, panels)
+    W = p.shape[1]
+    sh = np.zeros((world, cap, 2), np.uint64)
+    sp = np.zeros((world, cap, W), np.uint64)
+    sc = np.zeros(world, np.int64)
+    owner = (h[:, 0] % np.uint64(world)).astype(np.int64) if len(h) else np.zeros(0, np.int64)
+    for w in range(world):
+        sel = np.nonzero(owner == w)[0]
+        if len(sel) > cap:
+            raise RuntimeError("distinct-panel exchange: %d panels for owner %d exceed the segment capacity %d"
+                               % (len(sel), w, cap))
+        sh[w, : len(sel)] = h[sel]
+        sp[w, : len(sel)] = p[sel]
+        sc[w] = len(sel)
+    return sh, sp, sc
 
 
 def distinct_exact(hashes, panels):
@@ -100,6 +134,17 @@ def distinct_exact(hashes, panels):
         return 0
     h = np.asarray(hashes, np.uint64).reshape(len(p), 2)
     return int(len(np.unique(np.concatenate([h, p.reshape(len(p), -1)], axis=1), axis=0)))
+
+
+def distinct_segments(hashes, panels, counts):
+    """Host mirror of csa_unique_segments_async: distinct panels among the valid leading entries of
+    each segment (uint64[world, cap, 2], uint64[world, cap, W], counts[world])."""
+    h = np.asarray(hashes, np.uint64)
+    p = np.asarray(panels, np.uint64)
+    c = [int(x) for x in counts]
+    hv = np.concatenate([h[w, : c[w]] for w in range(len(c))]) if c else np.zeros((0, 2), np.uint64)
+    pv = np.concatenate([p[w, : c[w]] for w in range(len(c))]) if c else np.zeros((0, p.shape[-1]), np.uint64)
+    return distinct_exact(hv, pv)
 
 
 class HashTable:
@@ -128,45 +173,79 @@ def _host_collectives(t):
     return t.is_cuda and dist.get_backend() != "nccl"
 
 
-def exchange_panels(hashes, panels, W, stream=None):
-    """Send every panel (128-bit hash + W-word bitmask) to its owner rank h1 % world.
-
-    hashes: int64[2*S_local], panels: int64[S_local*W], both on the device (buckets from
-    csa_hash_buckets_async) or on the host (numpy bucketing).  Returns (hashes, panels) this rank
-    owns: int64[2*m], int64[m*W]."""
-    import torch
+def _all_to_all(out, inp):
+    """Equal-split all_to_all_single, through host copies for a gloo rehearsal on device tensors."""
     import torch.distributed as dist
-    world = dist.get_world_size()
-    n = hashes.numel() // 2
-    if hashes.is_cuda:
-        from . import _native as N
-        out_h = torch.empty_like(hashes)
-        out_p = torch.empty(max(n * W, 1), dtype=torch.int64, device=hashes.device)
-        counts = torch.empty(world, dtype=torch.int64, device=hashes.device)
-        cursor = torch.empty(world, dtype=torch.int64, device=hashes.device)
-        sp = ctypes.c_void_p((stream or torch.cuda.current_stream(hashes.device)).cuda_stream)
-        N.check(N.lib().csa_hash_buckets_async(N.ptr(hashes), N.ptr(panels), n, W, world, N.ptr(out_h),
-                                               N.ptr(out_p), N.ptr(counts), N.ptr(cursor), sp))
-        out_p = out_p[: n * W]
+    if _host_collectives(inp):
+        o = out.cpu()
+        dist.all_to_all_single(o, inp.cpu())
+        out.copy_(o)
     else:
-        h, p, c = owner_buckets(hashes.numpy().view(np.uint64), panels.numpy().view(np.uint64).reshape(n, W), world)
-        out_h = torch.from_numpy(np.ascontiguousarray(h).view(np.int64).reshape(-1))
-        out_p = torch.from_numpy(np.ascontiguousarray(p).view(np.int64).reshape(-1))
-        counts = torch.from_numpy(c)
-    via_host = _host_collectives(out_h)
-    send_counts = counts.cpu() if via_host else counts
-    recv_counts = torch.empty_like(send_counts)
-    dist.all_to_all_single(recv_counts, send_counts)
-    sc, rc = send_counts.tolist(), recv_counts.tolist()   # the exchange's one host synchronisation
-    src_h = out_h.cpu() if via_host else out_h
-    src_p = out_p.cpu() if via_host else out_p
-    recv_h = torch.empty(2 * sum(rc), dtype=torch.int64, device=src_h.device)
-    recv_p = torch.empty(W * sum(rc), dtype=torch.int64, device=src_p.device)
-    dist.all_to_all_single(recv_h, src_h, [2 * c for c in rc], [2 * c for c in sc])
-    dist.all_to_all_single(recv_p, src_p, [W * c for c in rc], [W * c for c in sc])
-    if via_host:
-        return recv_h.to(hashes.device), recv_p.to(hashes.device)
-    return recv_h, recv_p
+        dist.all_to_all_single(out, inp)
+
+
+class PanelExchange:
+    """The distinct-panel exchange of one rank, buffers sized once for n_local panels of W words.
+
+    ``run(hashes, panels, n, status, stream)`` returns this rank's owner count (a 1-element int64
+    tensor, device or host like the inputs); the caller all_reduces it.  Device inputs: no host
+    synchronisation (csa_exchange_pack_async -> three equal-split all_to_alls ->
+    csa_unique_segments_async), so a caller can enqueue the next steps behind it."""
+
+    def __init__(self, n_local, W, world, device):
+        import torch
+        from . import _native as N
+        self.W, self.world, self.device = int(W), int(world), device
+        self.n_local = max(int(n_local), 1)
+        self.cap = exchange_capacity(self.n_local, self.world)
+        self.cuda = torch.device(device).type == "cuda"
+        if not self.cuda:
+            return
+        i64 = torch.int64
+        seg = self.world * self.cap
+        self.send_h = torch.empty(2 * seg, dtype=i64, device=device)
+        self.send_p = torch.empty(seg * self.W, dtype=i64, device=device)
+        self.send_c = torch.zeros(self.world, dtype=i64, device=device)
+        self.recv_h = torch.empty_like(self.send_h)
+        self.recv_p = torch.empty_like(self.send_p)
+        self.recv_c = torch.zeros_like(self.send_c)
+        sb = int(N.lib().csa_exchange_scratch_bytes(self.n_local))
+        self.scratch = torch.empty((sb + 7) // 8, dtype=i64, device=device)
+        self.table = HashTable(seg, device)
+
+    def run(self, hashes, panels, n, status=None, stream=None):
+        import torch
+        n = int(n)
+        assert n <= self.n_local
+        if not hashes.is_cuda:
+            import torch.distributed as dist
+            sh, sp, sc = segment_buckets(hashes.numpy().view(np.uint64)[: 2 * n],
+                                         panels.numpy().view(np.uint64)[: n * self.W].reshape(n, self.W),
+                                         self.world, self.cap)
+            rh, rp, rc = (torch.empty(x.shape, dtype=torch.int64) for x in (sh, sp, sc))
+            dist.all_to_all_single(rc, torch.from_numpy(sc))
+            dist.all_to_all_single(rh, torch.from_numpy(sh.view(np.int64)))
+            dist.all_to_all_single(rp, torch.from_numpy(sp.view(np.int64)))
+            u = distinct_segments(rh.numpy().view(np.uint64), rp.numpy().view(np.uint64), rc.numpy())
+            return torch.tensor([u], dtype=torch.int64)
+        from . import _native as N
+        assert status is not None, "the device exchange reports a full segment in the status block"
+        st = stream or torch.cuda.current_stream(hashes.device)
+        sp_ = ctypes.c_void_p(st.cuda_stream)
+        L = N.lib()
+        N.check(L.csa_exchange_pack_async(N.ptr(hashes), N.ptr(panels), n, self.W, self.world, self.cap,
+                                          N.ptr(self.scratch), self.scratch.numel() * 8, N.ptr(self.send_h),
+                                          N.ptr(self.send_p), N.ptr(self.send_c), N.ptr(status), sp_))
+        with torch.cuda.stream(st):
+            _all_to_all(self.recv_c, self.send_c)
+            _all_to_all(self.recv_h, self.send_h)
+            _all_to_all(self.recv_p, self.send_p)
+            self.table.count.zero_()
+        N.check(L.csa_unique_segments_async(N.ptr(self.recv_h), N.ptr(self.recv_p), self.world, self.cap,
+                                            N.ptr(self.recv_c), self.W, N.ptr(self.table.table), self.table.slots,
+                                            N.ptr(self.table.count), N.ptr(status), sp_))
+        with torch.cuda.stream(st):
+            return self.table.count.clone()
 
 
 def _all_reduce_pairs(pairs, pair_bound, stream):
@@ -190,45 +269,42 @@ def _all_reduce_pairs(pairs, pair_bound, stream):
         dist.all_reduce(pairs, op=dist.ReduceOp.SUM)
 
 
-def _all_reduce(t):
+def _all_reduce(t, op=None):
     import torch.distributed as dist
+    op = dist.ReduceOp.SUM if op is None else op
     if _host_collectives(t):
         h = t.cpu()
-        dist.all_reduce(h, op=dist.ReduceOp.SUM)
+        dist.all_reduce(h, op=op)
         t.copy_(h)
     else:
-        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        dist.all_reduce(t, op=op)
 
 
-def combine(counts, pairs, hashes, panels, W, table=None, stream=None, pair_bound=None, status=None):
-    """Exchange steps for this rank; returns (counts, pairs, unique_tensor).
+def combine(counts, pairs, hashes, panels, W, exchange=None, stream=None, pair_bound=None, status=None):
+    """Exchange steps for this rank; returns (counts, pairs, unique_tensor), all stream-ordered.
 
     counts int64[n], pairs int64[n*n] or None, hashes int64[2*S_local] and panels
     int64[S_local*W] (this rank's panels).  Counts and pairs: all_reduce(SUM).  Distinct
-    panels: every panel goes to its owner rank (exchange_panels), the owner counts its distinct
-    panels exactly (device: csa_unique_async with bitmask comparison, table overflow reported in
-    ``status``; host: numpy), all_reduce(SUM) of the counts.
+    panels: ``exchange`` (a PanelExchange, built here if None) sends the local distinct panels
+    to their owners, each owner counts exactly, all_reduce(SUM) of the counts.
     """
     import torch
+    import torch.distributed as dist
+    n_local = hashes.numel() // 2
+    if exchange is None:
+        # every rank must size its segments alike (equal-split all_to_all): the largest shard's
+        n_max = torch.tensor([n_local], dtype=torch.int64, device=hashes.device)
+        _all_reduce(n_max, op=dist.ReduceOp.MAX)
+        exchange = PanelExchange(int(n_max.item()), W, dist.get_world_size(), hashes.device)
     _all_reduce(counts)
     if pairs is not None:
         _all_reduce_pairs(pairs, pair_bound, stream)
-    mine_h, mine_p = exchange_panels(hashes, panels, W, stream)
-    m = mine_h.numel() // 2
-    if mine_h.is_cuda:
-        from . import _native as N
-        if table is None:
-            table = HashTable(m, mine_h.device)
-        table.ensure(m)
-        table.count.zero_()
-        sp = ctypes.c_void_p((stream or torch.cuda.current_stream(mine_h.device)).cuda_stream)
-        N.check(N.lib().csa_unique_async(N.ptr(mine_h), N.ptr(mine_p), m, W, N.ptr(table.table), table.slots,
-                                         N.ptr(table.count), N.ptr(status), sp))
-        u = table.count.clone()
+    u = exchange.run(hashes, panels, n_local, status=status, stream=stream)
+    if u.is_cuda:
+        with torch.cuda.stream(stream or torch.cuda.current_stream(u.device)):
+            _all_reduce(u)
     else:
-        u = torch.tensor([distinct_exact(mine_h.numpy().view(np.uint64), mine_p.numpy().view(np.uint64).reshape(m, W))],
-                         dtype=torch.int64)
-    _all_reduce(u)
+        _all_reduce(u)
     return counts, pairs, u
 
 

@@ -240,16 +240,28 @@ int csa_unique_async(const uint64_t *d_hashes, const uint64_t *d_panels, uint64_
 int csa_pair_histogram_async(const int64_t *d_pairs, int32_t n, uint64_t *d_hist, uint64_t n_bins,
                              uint64_t *d_overflow, void *stream);
 
-/* Multi-GPU distinct-panel exchange, send side: bucket the 128-bit hashes (2*n_hashes uint64)
- * by owner rank h1 % world into d_out (2*n_hashes uint64, owner-major, any order inside a
- * bucket) and, with d_panels (n_hashes*W), the panels' bitmasks alongside into d_out_panels
- * (n_hashes*W, same order); d_counts (world uint64) = panels per owner, d_cursor (world uint64)
- * scratch.  The buckets feed an all_to_all; each owner then counts its distinct panels exactly
- * with csa_unique_async (equal panels have equal hashes, so they meet at one owner).
- * world <= 1024. */
-int csa_hash_buckets_async(const uint64_t *d_hashes, const uint64_t *d_panels, uint64_t n_hashes, int32_t W,
-                           uint32_t world, uint64_t *d_out, uint64_t *d_out_panels, uint64_t *d_counts,
-                           uint64_t *d_cursor, void *stream);
+/* Distinct panels over SEGMENTED input (the owner side of the multi-GPU exchange): n_segments
+ * segments of `capacity` entries each (hashes 2*capacity, panels capacity*W uint64 per segment),
+ * of which segment s holds d_seg_counts[s] (device uint64) valid leading entries.  Otherwise as
+ * csa_unique_async: *d_unique += the exact distinct count; table_slots >= 2*n_segments*capacity. */
+int csa_unique_segments_async(const uint64_t *d_hashes, const uint64_t *d_panels, uint32_t n_segments,
+                              uint64_t capacity, const uint64_t *d_seg_counts, int32_t W, uint64_t *d_table,
+                              uint64_t table_slots, uint64_t *d_unique, uint32_t *d_status, void *stream);
+
+/* Multi-GPU distinct-panel exchange, send side (no host synchronisation; replaces the reference's
+ * per-run `found_panels` set, analysis.py:171,186, across ranks).  The exact LOCAL distinct panels
+ * of d_hashes / d_panels (n_panels, hash AND bitmask equality) are bucketed by owner rank
+ * h1 % world into fixed-capacity segments: d_send_hashes uint64[world][capacity][2],
+ * d_send_panels uint64[world][capacity][W], d_send_counts uint64[world] (entries per segment;
+ * unused entries are left unwritten).  All three feed equal-split all_to_alls; the owner then calls
+ * csa_unique_segments_async on what it received.  A segment that would exceed `capacity` raises
+ * CSA_E_UNSUPPORTED in d_status (required).  d_scratch: csa_exchange_scratch_bytes(n_panels) bytes.
+ * world <= 1024, n_panels < 2^31. */
+uint64_t csa_exchange_scratch_bytes(uint64_t n_panels);
+int csa_exchange_pack_async(const uint64_t *d_hashes, const uint64_t *d_panels, uint64_t n_panels, int32_t W,
+                            uint32_t world, uint64_t capacity, void *d_scratch, uint64_t scratch_bytes,
+                            uint64_t *d_send_hashes, uint64_t *d_send_panels, uint64_t *d_send_counts,
+                            uint32_t *d_status, void *stream);
 
 /* Multi-GPU pair exchange: pack the upper triangle incl. the diagonal of the
  * n*n int64 pair counts row-major into n(n+1)/2 int32 (every count must be

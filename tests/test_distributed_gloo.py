@@ -2,13 +2,15 @@
 
 Each rank produces its contiguous shard of panels with the C oracle (standing in
 for that rank's GPU), then runs the real exchange code on host tensors: all_reduce
-of counts and pair counts, all_to_all of every panel (128-bit hash + bitmask) to
-its owner rank h1 % world through the host mirror of csa_hash_buckets_async, the
-owner's exact dedupe (host mirror of csa_unique_async: equal hash AND equal
-bitmask), all_reduce of the owners' counts.  The combined results must equal one
-unsharded run -- on an all-distinct instance and on a duplicate-heavy one whose
-duplicates land on different ranks -- and two different panels given the same
-128-bit hash must still count twice (the count is exact, not hash-based).
+of counts and pair counts; the rank's exact local distinct panels (128-bit hash +
+bitmask) in fixed-capacity segments per owner rank h1 % world (host mirror of
+csa_exchange_pack_async), three equal-split all_to_alls (segment counts, hashes,
+bitmasks), the owner's exact dedupe over the valid entries (host mirror of
+csa_unique_segments_async: equal hash AND equal bitmask), all_reduce of the
+owners' counts.  The combined results must equal one unsharded run -- on an
+all-distinct instance and on a duplicate-heavy one whose duplicates land on
+different ranks -- and two different panels given the same 128-bit hash must
+still count twice (the count is exact, not hash-based).
 """
 import os
 import socket
@@ -108,22 +110,35 @@ def test_gloo_exchange_exact_on_hash_collision(tmp_path):
     assert int(np.load(tmp_path / "unique.npy")[0]) == 2
 
 
-def test_owner_buckets_mirror():
-    """owner_buckets (host mirror of csa_hash_buckets_async): owner-major, every panel travels with
-    its hash, per-owner counts."""
+def test_segment_buckets_mirror():
+    """segment_buckets (host mirror of csa_exchange_pack_async): each owner segment holds exactly the
+    local DISTINCT panels it owns (h1 % world), every panel with its hash; capacity overflow raises."""
     D = pkg("distributed")
     rng = np.random.default_rng(3)
     p = rng.integers(0, 2 ** 63, size=(1000, 5), dtype=np.int64).astype(np.uint64)
+    p = np.concatenate([p, p[:300]])                       # 300 local duplicates
     h = D.panel_hashes(p)
     for world in (1, 2, 3, 8):
-        bh, bp, c = D.owner_buckets(h, p, world)
-        assert c.sum() == 1000 and len(c) == world
-        assert np.array_equal(D.panel_hashes(bp), bh)
-        start = 0
+        cap = D.exchange_capacity(len(p), world)
+        sh, sp, c = D.segment_buckets(h, p, world, cap)
+        assert c.sum() == 1000 and len(c) == world and c.max() <= cap
+        got = []
         for w in range(world):
-            assert np.all(bh[start:start + c[w], 0] % np.uint64(world) == np.uint64(w))
-            start += c[w]
-        assert sorted(map(tuple, bp.tolist())) == sorted(map(tuple, p.tolist()))
+            assert np.all(sh[w, : c[w], 0] % np.uint64(world) == np.uint64(w))
+            assert np.array_equal(D.panel_hashes(sp[w, : c[w]]), sh[w, : c[w]])
+            got += list(map(tuple, sp[w, : c[w]].tolist()))
+        assert sorted(got) == sorted(set(map(tuple, p.tolist())))
+        assert D.distinct_segments(sh, sp, c) == 1000
+    with pytest.raises(RuntimeError):
+        D.segment_buckets(h, p, 2, 100)
+
+
+def test_exchange_capacity_bounds():
+    D = pkg("distributed")
+    assert D.exchange_capacity(1, 8) == 1 and D.exchange_capacity(0, 8) == 1
+    assert D.exchange_capacity(1000, 1) == 1000
+    c = D.exchange_capacity(10 ** 6, 8)
+    assert 125000 < c < 128000          # mean + 8 sd + 64 of Binomial(1e6, 1/8)
 
 
 def test_distinct_exact_mirror():

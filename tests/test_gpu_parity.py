@@ -233,17 +233,54 @@ def test_device_pipeline_matches_host_api(gpu_available):
     torch.cuda.synchronize()
 
 
-def test_owner_partition_exact_on_device(gpu_available):
-    """Multi-GPU distinct-panel step on one device: csa_hash_buckets_async buckets panels (hash +
-    bitmask) by owner, csa_unique_async counts each owner's bucket exactly; the per-owner counts
-    sum to the global count for any world, and a forged hash collision between two different
-    panels still counts twice (bitmask comparison, not hash equality)."""
+def _exchange_on_device(h, p, W, world, shards, cap, status):
+    """The multi-GPU distinct-panel exchange with `world` simulated ranks on one device: each sender
+    packs its shard (csa_exchange_pack_async), the all_to_all is done by slicing, each owner counts
+    its segments (csa_unique_segments_async).  Returns (sum of owner counts, per-sender host copies
+    of (hashes, panels, counts) segments)."""
     import torch
     D = pkg("distributed")
     N = pkg("_native")
+    L = N.lib()
+    sends = []
+    for b, e in shards:
+        sh = torch.zeros(world * cap * 2, dtype=torch.int64, device="cuda")
+        sp = torch.zeros(world * cap * W, dtype=torch.int64, device="cuda")
+        sc = torch.zeros(world, dtype=torch.int64, device="cuda")
+        sb = int(L.csa_exchange_scratch_bytes(max(e - b, 1)))
+        scratch = torch.empty((sb + 7) // 8, dtype=torch.int64, device="cuda")
+        N.check(L.csa_exchange_pack_async(N.ptr(h[2 * b:]), N.ptr(p[b * W:]), e - b, W, world, cap, N.ptr(scratch),
+                                          scratch.numel() * 8, N.ptr(sh), N.ptr(sp), N.ptr(sc), N.ptr(status), None))
+        sends.append((sh, sp, sc))
+    torch.cuda.synchronize()
+    total = 0
+    table = D.HashTable(world * cap, h.device)
+    for r in range(world):
+        rh = torch.cat([sh[r * cap * 2:(r + 1) * cap * 2] for sh, _, _ in sends])
+        rp = torch.cat([sp[r * cap * W:(r + 1) * cap * W] for _, sp, _ in sends])
+        rc = torch.stack([sc[r] for _, _, sc in sends])
+        table.count.zero_()
+        N.check(L.csa_unique_segments_async(N.ptr(rh), N.ptr(rp), world, cap, N.ptr(rc), W, N.ptr(table.table),
+                                            table.slots, N.ptr(table.count), N.ptr(status), None))
+        torch.cuda.synchronize()
+        total += int(table.count.item())
+    host = [(sh.cpu().numpy().view(np.uint64).reshape(world, cap, 2), sp.cpu().numpy().view(np.uint64).reshape(world, cap, W),
+             sc.cpu().numpy()) for sh, sp, sc in sends]
+    return total, host
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 8])
+def test_exchange_exact_on_device(gpu_available, world):
+    """Multi-GPU distinct-panel exchange on one device (world simulated ranks, contiguous shards):
+    every sender's owner segments hold exactly its local DISTINCT panels (host mirror
+    segment_buckets), the owners' exact counts sum to the global distinct count with duplicates
+    split across senders, and a forged hash collision between two different panels still counts
+    twice (bitmask comparison, not hash equality)."""
+    import torch
+    D = pkg("distributed")
     o = oracle_read(*inst_paths("example_small_20"), 20)
     rc, panels, _, _ = coracle.draw(o, 20, 3, 0, 5000)
-    panels = np.concatenate([panels, panels[:700]])           # 700 duplicates
+    panels = np.concatenate([panels, panels[:700], panels[2000:2300]])     # duplicates, some in other shards
     W = panels.shape[1]
     hashes = D.panel_hashes(panels)
     hashes[1000] = hashes[0]              # forged collision: panel 1000 (no duplicate) differs from panel 0
@@ -252,28 +289,37 @@ def test_owner_partition_exact_on_device(gpu_available):
     assert want == 5000
     h = torch.from_numpy(hashes.ravel().view(np.int64).copy()).cuda()
     p = torch.from_numpy(panels.ravel().view(np.int64).copy()).cuda()
-    m = len(panels)
     status = torch.zeros(4, dtype=torch.int32, device="cuda")
-    for world in (1, 2, 3, 8):
-        out_h, out_p = torch.empty_like(h), torch.empty_like(p)
-        counts = torch.empty(world, dtype=torch.int64, device="cuda")
-        cursor = torch.empty(world, dtype=torch.int64, device="cuda")
-        N.check(N.lib().csa_hash_buckets_async(N.ptr(h), N.ptr(p), m, W, world, N.ptr(out_h), N.ptr(out_p),
-                                               N.ptr(counts), N.ptr(cursor), None))
-        torch.cuda.synchronize()
-        c = counts.cpu().numpy()
-        starts = np.concatenate([[0], np.cumsum(c)])
-        table = D.HashTable(m, h.device)
-        total = 0
-        for r in range(world):
-            a, b = int(starts[r]), int(starts[r + 1])
-            table.count.zero_()
-            N.check(N.lib().csa_unique_async(N.ptr(out_h[2 * a:]), N.ptr(out_p[a * W:]), b - a, W, N.ptr(table.table),
-                                             table.slots, N.ptr(table.count), N.ptr(status), None))
-            torch.cuda.synchronize()
-            total += int(table.count.item())
-        assert int(status[0].item()) == 0
-        assert total == want
+    shards = [D.shard_range(len(panels), world, r) for r in range(world)]
+    cap = D.exchange_capacity(max(e - b for b, e in shards), world)
+    total, host = _exchange_on_device(h, p, W, world, shards, cap, status)
+    assert int(status[0].item()) == 0
+    assert total == want
+    for (b, e), (sh, sp, sc) in zip(shards, host):
+        mh, mp, mc = D.segment_buckets(hashes[b:e], panels[b:e], world, cap)
+        assert sc.tolist() == mc.tolist()
+        for w in range(world):
+            got = sorted(map(tuple, np.concatenate([sh[w, : sc[w]], sp[w, : sc[w]]], axis=1).tolist()))
+            exp = sorted(map(tuple, np.concatenate([mh[w, : mc[w]], mp[w, : mc[w]]], axis=1).tolist()))
+            assert got == exp
+
+
+def test_exchange_overflow_raises(gpu_available):
+    """A segment past its capacity is an error in the status block (never a silently short count)."""
+    import torch
+    D = pkg("distributed")
+    N = pkg("_native")
+    rng = np.random.default_rng(5)
+    panels = rng.integers(0, 2 ** 63, size=(1000, 3), dtype=np.int64).astype(np.uint64)
+    hashes = D.panel_hashes(panels)
+    h = torch.from_numpy(hashes.ravel().view(np.int64).copy()).cuda()
+    p = torch.from_numpy(panels.ravel().view(np.int64).copy()).cuda()
+    status = torch.zeros(4, dtype=torch.int32, device="cuda")
+    _exchange_on_device(h, p, 3, 2, [(0, 1000)], 100, status)
+    st = status.cpu().numpy().astype(np.uint32)
+    assert st[0] == N.CSA_E_UNSUPPORTED
+    with pytest.raises(N.CsaError):
+        N.check(N.lib().csa_status_decode(N.ptr(st)))
 
 
 def test_device_hashes_match_host_mirror(gpu_available):
@@ -287,41 +333,6 @@ def test_device_hashes_match_host_mirror(gpu_available):
     pipe.check_status()
     dev_h = pipe.hashes.cpu().numpy().view(np.uint64).reshape(-1, 2)
     assert np.array_equal(dev_h, D.panel_hashes(pipe.panels_view(4096)))
-
-
-@pytest.mark.parametrize("world", [1, 3, 8])
-def test_hash_buckets(gpu_available, world):
-    """csa_hash_buckets_async: owner-major buckets (h1 % world) holding exactly the input hashes,
-    each with its panel words alongside."""
-    import torch
-    N = pkg("_native")
-    rng = np.random.default_rng(world)
-    W = 3
-    h = rng.integers(0, 2 ** 63, size=(50001, 2), dtype=np.int64)
-    pn = np.concatenate([h, np.arange(50001, dtype=np.int64)[:, None]], axis=1)  # panel = (h1, h2, index)
-    d = torch.from_numpy(h.reshape(-1)).cuda()
-    dp = torch.from_numpy(pn.reshape(-1).copy()).cuda()
-    out = torch.empty_like(d)
-    outp = torch.empty_like(dp)
-    counts = torch.empty(world, dtype=torch.int64, device="cuda")
-    cursor = torch.empty(world, dtype=torch.int64, device="cuda")
-    N.check(N.lib().csa_hash_buckets_async(N.ptr(d), N.ptr(dp), 50001, W, world, N.ptr(out), N.ptr(outp),
-                                           N.ptr(counts), N.ptr(cursor), None))
-    torch.cuda.synchronize()
-    o = out.cpu().numpy().reshape(-1, 2).view(np.uint64)
-    op = outp.cpu().numpy().reshape(-1, W)
-    assert np.array_equal(op[:, :2].view(np.uint64), o)              # every panel travelled with its hash
-    assert sorted(op[:, 2].tolist()) == list(range(50001))
-    owner = h.view(np.uint64)[:, 0] % np.uint64(world)
-    c = counts.cpu().numpy()
-    assert c.tolist() == np.bincount(owner.astype(np.int64), minlength=world).tolist()
-    start = 0
-    for w in range(world):
-        seg = o[start:start + c[w]]
-        assert np.all(seg[:, 0] % np.uint64(world) == np.uint64(w))
-        want = h.view(np.uint64)[owner == np.uint64(w)]
-        assert sorted(map(tuple, seg.tolist())) == sorted(map(tuple, want.tolist()))
-        start += c[w]
 
 
 @pytest.mark.parametrize("n", [1, 7, 110, 257, 1727])

@@ -82,17 +82,25 @@ def test_shard_range_covers_exactly():
 
 
 def test_owner_partition_dedupe():
-    """Distinct panels summed over owner partitions (owner = h1 % world) == the global count, for
-    any world: equal panels have equal hashes, so they always meet at one owner."""
+    """Distinct panels summed over owner segments (owner = h1 % world) == the global count, for any
+    world: equal panels have equal hashes, so they always meet at one owner."""
     D = pkg("distributed")
     rng = np.random.default_rng(0)
     p = rng.integers(0, 2 ** 63, size=(500, 4), dtype=np.int64).astype(np.uint64)
     p = np.concatenate([p, p[:100]])                       # 100 duplicates
     h = D.panel_hashes(p)
     for world in (1, 2, 4, 7):
-        bh, bp, c = D.owner_buckets(h, p, world)
-        starts = np.concatenate([[0], np.cumsum(c)])
-        total = sum(D.distinct_exact(bh[starts[r]:starts[r + 1]], bp[starts[r]:starts[r + 1]]) for r in range(world))
+        # the 600 panels split over `world` sender ranks, each sending its local distinct panels to
+        # their owners; owner r's count over the segments from every sender
+        shards = np.array_split(np.arange(len(p)), world)
+        cap = D.exchange_capacity(max(len(x) for x in shards), world)
+        segs = [D.segment_buckets(h[x], p[x], world, cap) for x in shards]
+        total = 0
+        for r in range(world):
+            rh = np.stack([sg[0][r] for sg in segs])
+            rp = np.stack([sg[1][r] for sg in segs])
+            rc = np.array([sg[2][r] for sg in segs])
+            total += D.distinct_segments(rh, rp, rc)
         assert total == 500
 
 
