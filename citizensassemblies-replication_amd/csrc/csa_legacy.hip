@@ -1883,6 +1883,19 @@ int csa_pairs_unpack_async(const int32_t *d_packed, int32_t n, int64_t *d_pairs,
     return CSA_OK;
 }
 
+#ifdef CSA_LANE_STAMPS
+// diagnostic builds only: the draw_lane_kernel segment totals (cycles summed over waves, [8] = waves)
+int csa_debug_lane_stamps(uint64_t *out16, int reset) {
+    HIPCHK(hipDeviceSynchronize());
+    HIPCHK(hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_lane_stamps), 16 * 8));
+    if (reset) {
+        static const unsigned long long zero[16] = {};
+        HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_lane_stamps), zero, 16 * 8));
+    }
+    return CSA_OK;
+}
+#endif
+
 int csa_status_decode(const uint32_t *h) {
     if (!h) return fail(CSA_E_INVALID, "null status");
     const uint64_t panel = (uint64_t)h[1] | ((uint64_t)h[2] << 32);
