@@ -190,6 +190,21 @@ def cpu_baseline(inst_dir, k, seed, target_s, want_pairs):
     return out
 
 
+def load_valu_peak():
+    """Integer VALU issue roof of one MI355X (wave-instructions/s over the chip): tools/valu_rate.hip
+    on the GPU box, 8 waves/SIMD of independent v_add_u32 / v_bcnt / v_cndmask / v_mul_i32_i24_sdwa
+    chains (profiles/valu_rate_mi355x.jsonl).  A wave64 integer VALU instruction occupies its SIMD
+    ~4.3 cycles at the 2.4 GHz peak clock, not the 2 of an f32 FMA's nominal rate."""
+    path = os.path.join(REPO, "profiles", "valu_rate_mi355x.jsonl")
+    if not os.path.exists(path):
+        return None
+    with open(path) as fh:
+        rows = [json.loads(line) for line in fh if line.strip()]
+    ints = [r["wave_inst_per_s_chip"] for r in rows if r["op"] != "v_fma_f32"]
+    return {"peak_wave_inst_per_s": sum(ints) / len(ints), "source": "profiles/valu_rate_mi355x.jsonl",
+            "ops": {r["op"]: r["wave_inst_per_s_chip"] for r in rows}} if ints else None
+
+
 def load_pmc(config):
     """Committed rocprofv3 --pmc summary (tools/make_pmc_profile.py) for this config."""
     path = os.path.join(REPO, "profiles", "pmc_%s.json" % config)
@@ -477,13 +492,26 @@ def main():
         roof = {"kernel": name, "bound": "hbm", "achieved": ach, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
                 "frac": ach * 1e9 / HBM_PEAK, "traffic": traffic, "algorithmic_bytes": b}
         if dominant == "draw":
-            roof["note"] = ("the draw kernel has no HBM or MFMA roof: it is VALU/LDS issue-bound; 'achieved' is "
-                            "its algorithmic writes (2k B of pick list per panel) over its in-region time; "
-                            "issue_frac / mean_waves_per_simd come from rocprofv3 PMC passes of these kernel sources")
+            roof["note"] = ("the draw kernel has no HBM or MFMA roof: it is bound by VALU issue; 'achieved' is its "
+                            "algorithmic writes (2k B of pick list per panel) over its in-region time (the HBM "
+                            "framing the contract asks for); roofline.valu is the binding roof: its VALU "
+                            "wave-instructions per second (rocprofv3 SQ_INSTS_VALU of these sources) over the "
+                            "integer VALU issue rate measured on the chip (tools/valu_rate.hip); issue_frac_2cyc "
+                            "is the same count priced at 2 cycles per wave-instruction, which integer VALU does "
+                            "not reach")
             if pmc_ok and pmc.get("draw_issue") and pmc.get("draw_kernel") == draw_name:
                 kernels["draw"]["pmc_issue"] = pmc["draw_issue"]
-                roof["issue_frac"] = pmc["draw_issue"].get("valu_issue_frac")
+                roof["issue_frac_2cyc"] = pmc["draw_issue"].get("valu_issue_frac")
                 roof["mean_waves_per_simd"] = pmc["draw_issue"].get("mean_waves_per_simd")
+                # the roof that binds: VALU instructions of this kernel (PMC, same sources) per second
+                # in the timed region vs the measured integer VALU issue rate of the chip
+                vp = load_valu_peak()
+                if vp and stage_pipe["draw"] > 0:
+                    rate = pmc["draw_issue"]["valu_insts_per_panel"] * S / (stage_pipe["draw"] * 1e-3)
+                    roof["valu"] = {"bound": "valu_issue", "achieved": rate, "peak": vp["peak_wave_inst_per_s"],
+                                    "unit": "wave-instructions/s", "frac": rate / vp["peak_wave_inst_per_s"],
+                                    "valu_insts_per_panel": pmc["draw_issue"]["valu_insts_per_panel"],
+                                    "peak_source": vp["source"]}
     roof["pmc_source_sha"] = sha
     roof["pmc_matches_sources"] = pmc_ok
 

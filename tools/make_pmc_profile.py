@@ -59,6 +59,10 @@ def main():
                 issue["valu_issue_frac"] = c["SQ_INSTS_VALU"] * 2 / (SIMDS * gui / 8)
                 if ns:
                     issue["clock_GHz"] = gui / 8 / (ns * 1e-9) / 1e9
+            if gui and c.get("SQ_ACTIVE_INST_VALU"):
+                # SQ_ACTIVE_INST_VALU counts quad-cycles: the fraction of SIMD cycles with a VALU
+                # instruction of this kernel in flight (~1 = the VALU pipe never idles)
+                issue["valu_active_frac"] = c["SQ_ACTIVE_INST_VALU"] * 4 / (SIMDS * gui / 8)
             if c.get("SQ_ACTIVE_INST_LDS"):
                 issue["lds_bank_conflict_per_active_lds"] = c.get("SQ_LDS_BANK_CONFLICT", 0) / c["SQ_ACTIVE_INST_LDS"]
             if c.get("SQ_WAVE_CYCLES"):
