@@ -1234,6 +1234,7 @@ struct csa_instance {
     int32_t max_abs = 0;  // max |fmin| / |sel0| bound for the cross-multiplication range check
     bool zero_max_min = false;  // some feature has max 0 and min > 0 (draw_batch_kernel excludes it)
     bool sel_over_max = false;  // some feature starts with selected > max (draw_lane_kernel excludes it)
+    int32_t max_slack = 0;      // max over live features of max - selected (draw_lane_kernel: <= 255)
     // grow-only device scratch + a stream for the repeated small host-API calls
     // (csa_first_panel_not_in: XMIN calls it 5n times)
     void *scratch[24] = {};   // slots 0-7: csa_first_panel_not_in; 8-23: csa_legacy_sample
@@ -1378,7 +1379,7 @@ int pow2_ceil_int(int x) {
 int pick_draw_config(const csa_instance *I, bool general, DrawConfig &c) {
     general = general || I->d_addr_next;  // same-address deletions: draw_kernel<64, ..., true> only
     const bool lane_ok = I->F <= 32 && I->d_pmask && !I->zero_max_min && I->W <= 32 && I->max_abs < 32768 &&
-                         !I->sel_over_max;
+                         !I->sel_over_max && I->max_slack <= 255;
     const bool wide_ok = I->F <= 64 && I->W <= 128 && !I->zero_max_min && I->max_abs < 32768 && !I->sel_over_max;
     const bool g16_ok = I->F <= 64 && I->W <= 256;
     int choice = general ? 64 : lane_ok ? 2 : wide_ok ? 8 : g16_ok ? 16 : 64;
@@ -1719,6 +1720,7 @@ int csa_instance_create(int32_t n, int32_t C, int32_t F, const int32_t *person_f
         }
     for (int f = 0; f < F; ++f) {
         I->max_abs = std::max(I->max_abs, std::abs(fmin[f]));
+        if (fmax[f] > 0) I->max_slack = std::max(I->max_slack, fmax[f]);
         if (fmax[f] == 0 && fmin[f] != 0) I->zero_max_min = true;
         if (feat_cat[f] < 0 || feat_cat[f] >= C) {
             delete I;
@@ -1813,11 +1815,13 @@ int csa_instance_set_state(csa_instance *I, const int32_t *sel, const int32_t *r
     int32_t mx = 0;
     for (int f = 0; f < I->F; ++f) mx = std::max(mx, std::abs(I->fmin[f]));
     I->sel_over_max = false;
-    if (sel)
-        for (int f = 0; f < I->F; ++f) {
-            mx = std::max(mx, std::abs(sel[f]));
-            if (sel[f] > I->fmax[f]) I->sel_over_max = true;
-        }
+    I->max_slack = 0;
+    for (int f = 0; f < I->F; ++f) {
+        const int32_t s = sel ? sel[f] : 0;
+        if (sel) mx = std::max(mx, std::abs(s));
+        if (s > I->fmax[f]) I->sel_over_max = true;
+        if (I->fmax[f] > 0) I->max_slack = std::max(I->max_slack, I->fmax[f] - s);
+    }
     I->max_abs = mx;
     if (present)
         for (int w = 0; w < I->W; ++w)
