@@ -63,9 +63,10 @@ def parse():
                     help="serialise every stage on one stream (default: draws on their own stream, "
                          "--bufs - 1 steps ahead of the counting)")
     ap.add_argument("--bufs", type=int, default=3, help="panel buffers of the draw/count pipeline")
-    ap.add_argument("--pack-on", default="draw", choices=("draw", "count"),
-                    help="stream of picks_pack_kernel: after the draw on the draw stream, or first on the "
-                         "counting stream (one pick-list buffer per panel buffer)")
+    ap.add_argument("--pack-on", default="fused", choices=("fused", "draw", "count"),
+                    help="where pick lists become panels: inside the draw kernel (fused, default), "
+                         "picks_pack_kernel after the draw on the draw stream, or first on the counting "
+                         "stream (one pick-list buffer per panel buffer)")
     ap.add_argument("--iso-steps", type=int, default=2,
                     help="serial steps after the timed region that measure each kernel alone (not in `value`)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -200,7 +201,7 @@ def load_valu_peak():
         return None
     with open(path) as fh:
         rows = [json.loads(line) for line in fh if line.strip()]
-    ints = [r["wave_inst_per_s_chip"] for r in rows if r["op"] != "v_fma_f32"]
+    ints = [r["wave_inst_per_s_chip"] for r in rows if r["op"] in ("v_add_u32", "v_bcnt", "v_cndmask", "v_mul24_sdwa")]
     return {"peak_wave_inst_per_s": sum(ints) / len(ints), "source": "profiles/valu_rate_mi355x.jsonl",
             "ops": {r["op"]: r["wave_inst_per_s_chip"] for r in rows}} if ints else None
 
@@ -277,7 +278,7 @@ def main():
     pipe = Dv.DevicePipeline(enc, k, S, want_pairs=want_pairs, want_unique=True, device=dev, stream=stream,
                              pair_engine=engine_id)
     draw_name = pipe.draw_kernel_name()   # the kernel csa_draw_async launches (matches rocprofv3 names)
-    split = pipe.split_draw
+    split = pipe.split_draw and args.pack_on != "fused"   # separate pick-list draw + pack kernels
     W = enc.W
     # distinct-panel exchange buffers (fixed-capacity owner segments: no host sync per step)
     xchg = Dd.PanelExchange(S, W, world, dev) if world > 1 else None

@@ -1557,11 +1557,18 @@ int launch_draw(const csa_instance *I, int32_t k, uint64_t seed, uint64_t panel_
         HIPCHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, I->device));
         grid = std::min(want, (uint64_t)std::max(per_cu, 1) * (uint64_t)std::max(cus, 1));
     }
+    // the lane kernel packs its own panels (one workgroup per 128 panels, so every workgroup knows
+    // its panel range); the wide kernel's pick lists are packed by picks_pack_kernel
+    const bool fused = cfg.lane && !d_picks_ext && d_panels;
+    if (cfg.lane && !fused) {
+        A.panels = nullptr;
+        A.hashes = nullptr;
+    }
     void *args[] = {&A};
     HIPCHK(hipLaunchKernel(cfg.fn, dim3((unsigned)std::max<uint64_t>(1, grid)), dim3(threads), args, lds, stream));
     HIPCHK(hipGetLastError());
     if (cfg.picks() && !d_picks_ext) {  // pick lists -> packed panels (+ hashes)
-        if ((rc = launch_pack(A.picks16, n_panels, k, I->W, d_panels, d_hashes, stream))) return rc;
+        if (!fused && (rc = launch_pack(A.picks16, n_panels, k, I->W, d_panels, d_hashes, stream))) return rc;
         HIPCHK(hipEventRecord(M->picks_done, stream));
         M->picks_pending = true;
     }

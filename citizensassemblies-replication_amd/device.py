@@ -4,9 +4,11 @@ PyTorch only provides device memory, the stream and (in distributed.py) the
 RCCL collectives; every kernel is the hand-written HIP in csrc/.  One
 ``run`` = one pass of analysis.py:162-191 over a shard of panels:
 
-    draw_lane_kernel   panels [panel_begin, panel_begin+S) -> pick lists       (draw_picks)
-    picks_pack_kernel  pick lists -> packed bitmasks + 128-bit panel hashes    (pack)
-      (instances beyond the lane kernel: draw_kernel writes bitmasks + hashes directly)
+    draw_lane_kernel   panels [panel_begin, panel_begin+S) -> pick lists, then (in the same
+                       kernel, per workgroup) packed bitmasks + 128-bit panel hashes   (draw)
+    picks_pack_kernel  pick lists -> bitmasks + hashes for the wide kernel, or after
+                       draw_picks (the split form, kept for A/B)                        (pack)
+      (instances beyond both: draw_kernel writes bitmasks + hashes directly)
     xt_count_kernel    bitmasks -> transposed panel-indicator bits + per-person counts (+=)
     pair_mfma_kernel   transposed bits -> int32 partial blocks of X^T X on fp4 (default) or
     pair_reduce_kernel   int8 MFMA -> pair counts (+=, or = with overwrite)  (if want_pairs)
@@ -97,10 +99,8 @@ class DevicePipeline:
         batch with this batch's counting swaps ``self.panels`` / ``self.hashes`` between buffers
         and orders the streams with events (bench.py)."""
         assert S <= self.max_panels and self.panels.numel() >= S * self.enc.W
-        if self.split_draw:
-            self.draw_picks(seed, panel_begin, S, max_attempts, stream)
-            self.pack(S, stream)
-            return
+        # lane-kernel instances pack their panels inside the draw kernel (fused); the wide kernel's
+        # pick lists are packed by picks_pack_kernel inside the same call
         N.check(N.lib().csa_draw_async(self.enc.handle, self.k, int(seed) & 0xFFFFFFFFFFFFFFFF, int(panel_begin),
                                        int(S), max_attempts, N.ptr(self.panels), N.ptr(self.hashes),
                                        N.ptr(self.attempts), None, N.ptr(self.status),
