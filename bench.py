@@ -494,12 +494,13 @@ def main():
                 "frac": ach * 1e9 / HBM_PEAK, "traffic": traffic, "algorithmic_bytes": b}
         if dominant == "draw":
             roof["note"] = ("the draw kernel has no HBM or MFMA roof: it is bound by VALU issue; 'achieved' is its "
-                            "algorithmic writes (2k B of pick list per panel) over its in-region time (the HBM "
+                            "algorithmic output bytes (%s) over its in-region time (the HBM "
                             "framing the contract asks for); roofline.valu is the binding roof: its VALU "
                             "wave-instructions per second (rocprofv3 SQ_INSTS_VALU of these sources) over the "
                             "integer VALU issue rate measured on the chip (tools/valu_rate.hip); issue_frac_2cyc "
                             "is the same count priced at 2 cycles per wave-instruction, which integer VALU does "
-                            "not reach")
+                            "not reach") % ("2k B of pick list per panel" if split else
+                                             "8W + 16 B of packed panel and hash per panel")
             if pmc_ok and pmc.get("draw_issue") and pmc.get("draw_kernel") == draw_name:
                 kernels["draw"]["pmc_issue"] = pmc["draw_issue"]
                 roof["issue_frac_2cyc"] = pmc["draw_issue"].get("valu_issue_frac")
@@ -512,6 +513,7 @@ def main():
                     roof["valu"] = {"bound": "valu_issue", "achieved": rate, "peak": vp["peak_wave_inst_per_s"],
                                     "unit": "wave-instructions/s", "frac": rate / vp["peak_wave_inst_per_s"],
                                     "valu_insts_per_panel": pmc["draw_issue"]["valu_insts_per_panel"],
+                                    "pmc_valu_active_frac": pmc["draw_issue"].get("valu_active_frac"),
                                     "peak_source": vp["source"]}
     roof["pmc_source_sha"] = sha
     roof["pmc_matches_sources"] = pmc_ok

@@ -47,6 +47,11 @@ def main():
             e["write_bytes"] = c["WRITE_SIZE"] * 1024
         if "fetch_bytes_x2" in e and "write_bytes" in e:
             e["hbm_bytes_per_launch"] = e["fetch_bytes_x2"] + e["write_bytes"]
+            if e.get("avg_ns"):
+                e["hbm_GBps"] = e["hbm_bytes_per_launch"] / e["avg_ns"]
+        if c.get("SQ_VALU_MFMA_BUSY_CYCLES") and c.get("GRBM_GUI_ACTIVE"):
+            # MFMA pipe busy cycles summed over the SIMDs / (1024 SIMDs x the kernel's cycles)
+            e["mfma_busy_frac"] = c["SQ_VALU_MFMA_BUSY_CYCLES"] / (SIMDS * c["GRBM_GUI_ACTIVE"] / 8)
         if k.startswith("draw") and "SQ_INSTS_VALU" in c:
             draw_name = k
             gui = c.get("GRBM_GUI_ACTIVE")
