@@ -1233,7 +1233,9 @@ struct csa_instance {
     int32_t *d_addr_next = nullptr;  // same-address rings (csa_instance_set_address) or null
     int32_t max_abs = 0;  // max |fmin| / |sel0| bound for the cross-multiplication range check
     bool zero_max_min = false;  // some feature has max 0 and min > 0 (draw_batch_kernel excludes it)
-    bool sel_over_max = false;  // some feature starts with selected > max (draw_lane_kernel excludes it)
+    // some feature starts with selected >= max > 0: the lane / wide kernels test "selected == max" as
+    // need < min - max + 1 (true past max too), so such start states take draw_kernel (exact ==)
+    bool sel_over_max = false;
     int32_t max_slack = 0;      // max over live features of max - selected (draw_lane_kernel: <= 255)
     // grow-only device scratch + a stream for the repeated small host-API calls
     // (csa_first_panel_not_in: XMIN calls it 5n times)
@@ -1826,7 +1828,7 @@ int csa_instance_set_state(csa_instance *I, const int32_t *sel, const int32_t *r
     for (int f = 0; f < I->F; ++f) {
         const int32_t s = sel ? sel[f] : 0;
         if (sel) mx = std::max(mx, std::abs(s));
-        if (s > I->fmax[f]) I->sel_over_max = true;
+        if (s > I->fmax[f] || (I->fmax[f] > 0 && s == I->fmax[f])) I->sel_over_max = true;
         if (I->fmax[f] > 0) I->max_slack = std::max(I->max_slack, I->fmax[f] - s);
     }
     I->max_abs = mx;

@@ -489,3 +489,43 @@ def test_n16384_boundary(gpu_available):
     X = torch.from_numpy(np.unpackbits(opanels.view(np.uint8), axis=1, bitorder="little")[:, :n]).cuda().float()
     ref = (X.T @ X).to(torch.int64).cpu().numpy()
     assert np.array_equal(np.triu(raw.pairs), np.triu(ref))
+
+
+@pytest.mark.parametrize("name,k,S", [("sf_e_110", 110, 160), ("example_large_200", 200, 60)])
+def test_sample_from_state_at_max(gpu_available, name, k, S):
+    """A start state (the dicts' own "selected" counters, analysis.py:147-148) in which a feature
+    already sits at its max: its holders stay in the pool, picking one takes it past max, and no
+    cascade follows (legacy.py:113-114 tests ==).  The batch draw must route such a state to the
+    exact-equality kernel; panels equal the Python oracle's loop from the same state."""
+    import copy
+    A = pkg("analysis")
+    P = pkg()
+    inst, _ = _enc(name, k)
+    o = oracle_read(*inst_paths(name), k)
+    cats = copy.deepcopy(inst.categories)
+    # the live feature with the most holders whose max is reached
+    pool = o.pool_counts()
+    g = max((f for f in range(o.F) if o.fmax[f] > 0), key=lambda f: pool[f])
+    c, v = o.feat_names[g]
+    cats[c][v]["selected"] = o.fmax[g]
+    enc = P.encode(cats, inst.agents)
+    assert enc.feat_keys[g] == (c, v) and enc.sel0[g] == o.fmax[g]
+    seed = 17
+    raw = A.legacy_sample_raw(enc, k, S, seed, want_pairs=False, want_panels=True, want_attempts=True)
+    sel0 = [0] * o.F
+    sel0[g] = o.fmax[g]
+    src = PhiloxRng(seed)
+    rows = []
+    for panel in range(S):
+        a = 0
+        while True:
+            st, picks, sel, _, _ = draw_attempt(o, k, src.for_attempt(panel, a), sel=sel0)
+            if st == 0 and all(sel[f] >= o.fmin[f] for f in range(o.F)):
+                break
+            a += 1
+        row = np.zeros(enc.W, np.uint64)
+        for p_ in picks:
+            row[p_ >> 6] |= np.uint64(1) << np.uint64(p_ & 63)
+        rows.append(row)
+        assert raw.attempts[panel] == a + 1
+    assert np.array_equal(raw.panels, np.stack(rows))
