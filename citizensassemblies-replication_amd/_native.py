@@ -47,6 +47,8 @@ SIGNATURES = {
     "csa_instance_info": (ctypes.c_int, [_P, _P, _P, _P, _P]),
     "csa_instance_set_state": (ctypes.c_int, [_P, _P, _P, _P]),
     "csa_legacy_sample": (ctypes.c_int, [_P, _I32, _U64, _U64, _U64, _U32, _U32, _P, _P, _P, _P, _P]),
+    "csa_legacy_sample_devices": (ctypes.c_int, [_P, _P, _I32, _I32, _U64, _U64, _U64, _U32, _U32, _P, _P, _P,
+                                                 _P, _P]),
     "csa_legacy_find": (ctypes.c_int, [_P, _I32, _U64, _U64, _U64, _U32, _P, _P]),
     "csa_legacy_attempt": (ctypes.c_int, [_P, _I32, _U64, _U64, _U32, _P, _P, _P, _P, _P]),
     "csa_first_panel_not_in": (ctypes.c_int, [_P, _I32, _U64, _U64, _U64, _U32, _P, _U64, _U64, _P, _P]),

@@ -225,8 +225,10 @@ class LegacyRaw:
 
 
 def legacy_sample_raw(enc, k, iterations, random_seed, panel_begin=0, want_pairs=True, want_panels=True,
-                      want_attempts=False, max_attempts=0):
-    """Run the whole batch through csa_legacy_sample and return integer results."""
+                      want_attempts=False, max_attempts=0, devices=None):
+    """Run the whole batch through csa_legacy_sample and return integer results.  ``devices``
+    (a list of HIP device ids, repeats allowed) shards the panels over those devices of this
+    process through csa_legacy_sample_devices; the results are identical."""
     S = int(iterations)
     flags = N.CSA_WANT_COUNTS | N.CSA_WANT_UNIQUE
     counts = np.zeros(enc.n, np.int64)
@@ -238,9 +240,14 @@ def legacy_sample_raw(enc, k, iterations, random_seed, panel_begin=0, want_pairs
         flags |= N.CSA_WANT_PAIRS
     if want_panels:
         flags |= N.CSA_WANT_PANELS
-    rc = N.lib().csa_legacy_sample(enc.handle, int(k), int(random_seed) & 0xFFFFFFFFFFFFFFFF, panel_begin, S, flags,
-                                   max_attempts, N.ptr(panels), N.ptr(counts), N.ptr(pairs), N.ptr(unique),
-                                   N.ptr(attempts))
+    seed64 = int(random_seed) & 0xFFFFFFFFFFFFFFFF
+    outs = (N.ptr(panels), N.ptr(counts), N.ptr(pairs), N.ptr(unique), N.ptr(attempts))
+    if devices is None:
+        rc = N.lib().csa_legacy_sample(enc.handle, int(k), seed64, panel_begin, S, flags, max_attempts, *outs)
+    else:
+        dev = np.ascontiguousarray(devices, np.int32)
+        rc = N.lib().csa_legacy_sample_devices(enc.handle, N.ptr(dev), len(dev), int(k), seed64, panel_begin, S,
+                                               flags, max_attempts, *outs)
     if rc == N.CSA_E_BAD_QUOTAS:
         raise AssertionError(N.last_error())     # analysis.py:174-176
     if rc == N.CSA_E_NO_CANDIDATE:
@@ -305,7 +312,8 @@ def legacy_sample_device(enc, k, S, random_seed, keep_panels=True, chunk=1 << 20
 
 
 def legacy_probabilities(instance: Instance, iterations: int, random_seed: int,
-                         keep_panels: bool = True, rng: str = None) -> Tuple[ProbAllocation, PanelSet, PairHistogram]:
+                         keep_panels: bool = True, rng: str = None,
+                         devices=None) -> Tuple[ProbAllocation, PanelSet, PairHistogram]:
     """analysis.py:162-191 on the GPU.
 
     Returns ``({agent_id: count/S}, found_panels, pair_histogram)`` with the
@@ -318,6 +326,9 @@ def legacy_probabilities(instance: Instance, iterations: int, random_seed: int,
     drawn on the host from the stdlib MT19937 state exactly as legacy.py:149
     consumes it (csa_legacy_draw_mt) and counted / paired / deduplicated on the
     device.  It matches the published reference_output probabilities.
+
+    ``devices`` (Philox mode, one process): shard the panels over these HIP
+    devices through csa_legacy_sample_devices instead of torch.distributed.
     """
     from . import distributed as D
     mode = rng or _legacy.RNG_MODE
@@ -338,6 +349,10 @@ def legacy_probabilities(instance: Instance, iterations: int, random_seed: int,
     seed(random_seed)
     enc.check_quotas(instance.k)
     STREAM.take_panels(S)
+    if devices is not None:
+        raw = legacy_sample_raw(enc, instance.k, S, random_seed, want_pairs=True, want_panels=keep_panels,
+                                devices=devices)
+        return finish(instance, enc, raw, S)
     raw = legacy_sample_device(enc, instance.k, S, random_seed, keep_panels=keep_panels)
     return finish(instance, enc, raw, S)
 

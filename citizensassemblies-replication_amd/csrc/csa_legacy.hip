@@ -1170,6 +1170,12 @@ __global__ __launch_bounds__(kXbThreads) void exchange_bucket_kernel(
 // packed row-major into int32 (valid while every count < 2^31), so the all-reduce moves n(n+1)/2
 // words of 4 B instead of n^2 of 8 B (6 MB instead of 24 MB at sf_e); unpack writes them back.
 __device__ __forceinline__ uint64_t tri_offset(int i, int n) { return (uint64_t)i * n - (uint64_t)i * (i - 1) / 2; }
+// dst[i] += src[i] (csa_legacy_sample_devices: shard counts / pairs summed on shard 0's device)
+__global__ __launch_bounds__(256) void add_i64_kernel(int64_t *__restrict__ dst, const int64_t *__restrict__ src,
+                                                      uint64_t m) {
+    for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < m; i += (uint64_t)gridDim.x * 256ull) dst[i] += src[i];
+}
+
 __global__ __launch_bounds__(256) void pairs_pack_kernel(const int64_t *__restrict__ pairs, int n,
                                                          int32_t *__restrict__ packed) {
     const int i = blockIdx.x;
@@ -1239,8 +1245,8 @@ struct csa_instance {
     int32_t max_slack = 0;      // max over live features of max - selected (draw_lane_kernel: <= 255)
     // grow-only device scratch + a stream for the repeated small host-API calls
     // (csa_first_panel_not_in: XMIN calls it 5n times)
-    void *scratch[24] = {};   // slots 0-7: csa_first_panel_not_in; 8-23: csa_legacy_sample
-    size_t scratch_bytes[24] = {};
+    void *scratch[32] = {};   // slots 0-7: csa_first_panel_not_in; 8-19: csa_legacy_sample; 20-29: _devices
+    size_t scratch_bytes[32] = {};
     hipStream_t stream = nullptr;
     hipStream_t sdraw = nullptr, spost = nullptr;  // csa_legacy_sample's pipeline
     hipEvent_t drawn = nullptr;
@@ -1249,6 +1255,13 @@ struct csa_instance {
     size_t picks_bytes = 0;
     hipEvent_t picks_done = nullptr;
     bool picks_pending = false;
+    // host copies of the draw state (empty = default) and address rings, bumped generation `gen`
+    // on every set: csa_legacy_sample_devices' per-shard replicas re-mirror them when it changes
+    std::vector<int32_t> rem0h, addr_h;
+    std::vector<uint64_t> present0h;
+    uint64_t gen = 1;
+    std::vector<csa_instance *> replicas;  // [shard] (null: the instance itself / not created)
+    std::vector<uint64_t> replica_gen;
 };
 
 namespace {
@@ -1585,7 +1598,7 @@ int read_status(const uint32_t *d_status, hipStream_t stream, uint32_t *h) {
 
 // csa_legacy_sample's pipeline chunk (panels): 2^20 = one bench step at sf_e
 constexpr uint64_t kSampleChunk = 1ull << 20;
-constexpr int kSampleSlot0 = 8, kScratchSlots = 24;          // instance scratch slots of csa_legacy_sample
+constexpr int kSampleSlot0 = 8, kScratchSlots = 32;          // instance scratch slots of csa_legacy_sample
 constexpr size_t kSampleKeepBytes = (size_t)8 << 30;          // kept across calls up to 8 GiB
 
 uint64_t pow2_at_least(uint64_t x) {
@@ -1803,6 +1816,8 @@ void csa_instance_destroy(csa_instance *I) {
     if (I->stream) (void)hipStreamDestroy(I->stream);
     if (I->sdraw) (void)hipStreamDestroy(I->sdraw);
     if (I->spost) (void)hipStreamDestroy(I->spost);
+    for (csa_instance *R : I->replicas)
+        if (R) csa_instance_destroy(R);
     delete I;
 }
 
@@ -1839,6 +1854,9 @@ int csa_instance_set_state(csa_instance *I, const int32_t *sel, const int32_t *r
     I->sel0.assign(sel ? sel : zeros.data(), (sel ? sel : zeros.data()) + I->F);
     HIPCHK(hipMemcpy(I->d_rem0, rem ? rem : I->pool.data(), I->F * 4, hipMemcpyHostToDevice));
     if (I->W) HIPCHK(hipMemcpy(I->d_present0, present ? present : all.data(), I->W * 8, hipMemcpyHostToDevice));
+    if (rem) I->rem0h.assign(rem, rem + I->F); else I->rem0h.clear();
+    if (present) I->present0h.assign(present, present + I->W); else I->present0h.clear();
+    ++I->gen;
     return CSA_OK;
 }
 
@@ -1849,6 +1867,8 @@ int csa_instance_set_address(csa_instance *I, const int32_t *addr_next) {
     if (!addr_next) {
         if (I->d_addr_next) HIPCHK(hipFree(I->d_addr_next));
         I->d_addr_next = nullptr;
+        I->addr_h.clear();
+        ++I->gen;
         return CSA_OK;
     }
     for (int p = 0; p < I->n; ++p)
@@ -1858,6 +1878,8 @@ int csa_instance_set_address(csa_instance *I, const int32_t *addr_next) {
         if (rc) return rc;
     }
     HIPCHK(hipMemcpy(I->d_addr_next, addr_next, (size_t)I->n * 4, hipMemcpyHostToDevice));
+    I->addr_h.assign(addr_next, addr_next + I->n);
+    ++I->gen;
     return CSA_OK;
 }
 
@@ -2144,15 +2166,8 @@ int csa_exchange_pack_async(const uint64_t *d_hashes, const uint64_t *d_panels, 
     return CSA_OK;
 }
 
-int csa_legacy_sample(csa_instance *I, int32_t k, uint64_t seed, uint64_t panel_begin, uint64_t n_panels,
-                      uint32_t flags, uint32_t max_attempts, uint64_t *panels_out, int64_t *person_counts,
-                      int64_t *pair_counts, uint64_t *unique_out, uint32_t *attempts_out) {
-    if (!I) return fail(CSA_E_INVALID, "null instance");
-    if ((flags & CSA_WANT_PANELS) && !panels_out) return fail(CSA_E_INVALID, "panels_out is NULL");
-    if ((flags & CSA_WANT_COUNTS) && !person_counts) return fail(CSA_E_INVALID, "person_counts is NULL");
-    if ((flags & CSA_WANT_PAIRS) && !pair_counts) return fail(CSA_E_INVALID, "pair_counts is NULL");
-    if ((flags & CSA_WANT_UNIQUE) && !unique_out) return fail(CSA_E_INVALID, "unique_out is NULL");
-    // analysis.py:174-176
+// analysis.py:174-176: sum(min) <= k <= sum(max) in every category
+static int check_quotas(const csa_instance *I, int32_t k) {
     for (int c = 0; c < I->C; ++c) {
         int64_t smin = 0, smax = 0;
         for (int f = 0; f < I->F; ++f)
@@ -2164,14 +2179,45 @@ int csa_legacy_sample(csa_instance *I, int32_t k, uint64_t seed, uint64_t panel_
             return fail(CSA_E_BAD_QUOTAS, "category %d: sum(min)=%lld, sum(max)=%lld, k=%d", c, (long long)smin,
                         (long long)smax, k);
     }
+    return CSA_OK;
+}
+
+// Every exit of a sample call leaves the instance's streams idle, so the next call may reuse the
+// buffers; a batch above kSampleKeepBytes of device memory frees its buffers again.
+static void sample_drain(csa_instance *I) {
     ScopedDevice sd(I->device);
+    if (I->sdraw) (void)hipStreamSynchronize(I->sdraw);
+    if (I->spost) (void)hipStreamSynchronize(I->spost);
+    size_t held = 0;
+    for (int j = kSampleSlot0; j < kScratchSlots; ++j) held += I->scratch_bytes[j];
+    if (held > kSampleKeepBytes)
+        for (int j = kSampleSlot0; j < kScratchSlots; ++j)
+            if (I->scratch[j]) {
+                (void)hipFree(I->scratch[j]);
+                I->scratch[j] = nullptr;
+                I->scratch_bytes[j] = 0;
+            }
+}
+
+// device results of one enqueued batch (instance scratch; valid until the next call)
+struct SampleRun {
+    uint64_t *panels = nullptr, *hashes = nullptr, *table = nullptr, *uniq = nullptr;
+    int64_t *counts = nullptr, *pairs = nullptr;
+    uint32_t *attempts = nullptr, *status = nullptr;
+    uint64_t slots = 0;
+    int next_slot = kSampleSlot0;  // first instance scratch slot the batch left free
+};
+
+// Enqueue one batch on the instance's two streams, no host synchronisation.  Chunked pipeline:
+// chunk c + 1 is drawn (sdraw) while chunk c is transposed, counted and paired (spost); panels and
+// hashes hold the whole batch, XT and the pair scratch one chunk.  count_unique: the exact distinct
+// count into r.uniq (else only the hashes are written, for the caller's own dedupe).  On return
+// spost is ordered after every draw.
+static int sample_enqueue(csa_instance *I, int32_t k, uint64_t seed, uint64_t panel_begin, uint64_t n_panels,
+                          uint32_t flags, uint32_t max_attempts, bool want_attempts, bool count_unique,
+                          SampleRun &r) {
     const int n = I->n, W = I->W;
     const int npad = csa_xt_pad(std::max(n, 1));
-    // Chunked two-stream pipeline: chunk c + 1 is drawn (stream sd) while chunk c is transposed,
-    // counted and paired (stream sp); the panels and hashes buffers hold the whole batch (output
-    // copy, exact distinct count at the end), XT and the pair scratch one chunk.  Streams, event
-    // and buffers belong to the instance and are reused by the next call (grow-only; a batch
-    // above kSampleKeepBytes of device memory frees its buffers again on return).
     uint64_t chunk = kSampleChunk;
     if (const char *e = getenv("CSA_SAMPLE_CHUNK")) chunk = std::max<uint64_t>(64, strtoull(e, nullptr, 10));
     chunk = std::min(chunk, std::max<uint64_t>(n_panels, 1));
@@ -2180,77 +2226,249 @@ int csa_legacy_sample(csa_instance *I, int32_t k, uint64_t seed, uint64_t panel_
     if (!I->spost) HIPCHK(hipStreamCreateWithFlags(&I->spost, hipStreamNonBlocking));
     if (!I->drawn) HIPCHK(hipEventCreateWithFlags(&I->drawn, hipEventDisableTiming));
     hipStream_t sdraw = I->sdraw, spost = I->spost;
-    struct Drain {  // every exit leaves both streams idle, so the next call may reuse the buffers
-        csa_instance *I;
-        ~Drain() {
-            (void)hipStreamSynchronize(I->sdraw);
-            (void)hipStreamSynchronize(I->spost);
-            size_t held = 0;
-            for (int j = kSampleSlot0; j < kScratchSlots; ++j) held += I->scratch_bytes[j];
-            if (held > kSampleKeepBytes)
-                for (int j = kSampleSlot0; j < kScratchSlots; ++j)
-                    if (I->scratch[j]) {
-                        (void)hipFree(I->scratch[j]);
-                        I->scratch[j] = nullptr;
-                        I->scratch_bytes[j] = 0;
-                    }
-        }
-    } drain{I};
     int rc;
-    const bool want_unique = flags & CSA_WANT_UNIQUE, want_pairs = flags & CSA_WANT_PAIRS;
+    const bool want_hashes = flags & CSA_WANT_UNIQUE, want_pairs = flags & CSA_WANT_PAIRS;
     const bool want_counts = flags & CSA_WANT_COUNTS;
-    const uint64_t slots = pow2_at_least(std::max<uint64_t>(2 * n_panels, 64));
+    r.slots = pow2_at_least(std::max<uint64_t>(2 * n_panels, 64));
     const uint64_t sb = want_pairs ? csa_pair_scratch_bytes(n, cblk, CSA_PAIR_FP4) : 0;
-    uint64_t *panels = nullptr, *hashes = nullptr, *xt = nullptr, *table = nullptr, *uniq = nullptr;
-    int64_t *counts = nullptr, *pairs = nullptr;
-    uint32_t *attempts = nullptr, *status = nullptr;
+    uint64_t *xt = nullptr;
     int32_t *pscratch = nullptr;
-    int sl = kSampleSlot0;
-    if ((rc = scratch(I, sl++, std::max<uint64_t>(n_panels, 1) * W, &panels)) || (rc = scratch(I, sl++, 4, &status)))
+    int &sl = r.next_slot;
+    if ((rc = scratch(I, sl++, std::max<uint64_t>(n_panels, 1) * W, &r.panels)) ||
+        (rc = scratch(I, sl++, 4, &r.status)))
         return rc;
-    if (want_unique && ((rc = scratch(I, sl++, 2 * std::max<uint64_t>(n_panels, 1), &hashes)) ||
-                        (rc = scratch(I, sl++, slots, &table)) || (rc = scratch(I, sl++, 1, &uniq))))
+    if (want_hashes && (rc = scratch(I, sl++, 2 * std::max<uint64_t>(n_panels, 1), &r.hashes))) return rc;
+    if (want_hashes && count_unique &&
+        ((rc = scratch(I, sl++, r.slots, &r.table)) || (rc = scratch(I, sl++, 1, &r.uniq))))
         return rc;
-    if (attempts_out && (rc = scratch(I, sl++, std::max<uint64_t>(n_panels, 1), &attempts))) return rc;
-    if ((want_counts || want_pairs) && (rc = scratch(I, sl++, (size_t)n, &counts))) return rc;
-    if (want_pairs && ((rc = scratch(I, sl++, cblk * npad, &xt)) || (rc = scratch(I, sl++, (size_t)n * n, &pairs)) ||
+    if (want_attempts && (rc = scratch(I, sl++, std::max<uint64_t>(n_panels, 1), &r.attempts))) return rc;
+    if ((want_counts || want_pairs) && (rc = scratch(I, sl++, (size_t)n, &r.counts))) return rc;
+    if (want_pairs && ((rc = scratch(I, sl++, cblk * npad, &xt)) || (rc = scratch(I, sl++, (size_t)n * n, &r.pairs)) ||
                        (rc = scratch(I, sl++, sb / sizeof(int32_t) + 1, &pscratch))))
         return rc;
-    HIPCHK(hipMemsetAsync(status, 0, 16, sdraw));
-    if (counts) HIPCHK(hipMemsetAsync(counts, 0, (size_t)n * 8, spost));
-    if (uniq) HIPCHK(hipMemsetAsync(uniq, 0, 8, spost));
+    HIPCHK(hipMemsetAsync(r.status, 0, 16, sdraw));
+    if (r.counts) HIPCHK(hipMemsetAsync(r.counts, 0, (size_t)n * 8, spost));
+    if (r.uniq) HIPCHK(hipMemsetAsync(r.uniq, 0, 8, spost));
     for (uint64_t off = 0; off < n_panels; off += chunk) {
         const uint64_t len = std::min(chunk, n_panels - off);
-        uint64_t *cp = panels + off * W;
+        uint64_t *cp = r.panels + off * W;
         // the draw also writes the panels' 128-bit hashes (picks_pack_kernel / draw_kernel)
         if ((rc = launch_draw(I, k, seed, panel_begin + off, len, max_attempts, 0, 0, cp,
-                              want_unique ? hashes + 2 * off : nullptr, attempts ? attempts + off : nullptr, nullptr,
-                              status, nullptr, nullptr, nullptr, sdraw)))
+                              r.hashes ? r.hashes + 2 * off : nullptr, r.attempts ? r.attempts + off : nullptr,
+                              nullptr, r.status, nullptr, nullptr, nullptr, sdraw)))
             return rc;
         HIPCHK(hipEventRecord(I->drawn, sdraw));
         HIPCHK(hipStreamWaitEvent(spost, I->drawn, 0));
-        if (counts && (rc = csa_transpose_count_async(cp, len, n, xt, counts, spost))) return rc;
+        if (r.counts && (rc = csa_transpose_count_async(cp, len, n, xt, r.counts, spost))) return rc;
         // the first chunk stores its pair counts (no n*n zero-fill), later chunks add theirs
-        if (pairs && (rc = csa_pair_counts_ex_async(xt, (len + 63) / 64, n, pairs,
-                                                    CSA_PAIR_FP4 | (off == 0 ? CSA_PAIR_OVERWRITE : 0u), pscratch,
-                                                    sb, spost)))
+        if (r.pairs && (rc = csa_pair_counts_ex_async(xt, (len + 63) / 64, n, r.pairs,
+                                                      CSA_PAIR_FP4 | (off == 0 ? CSA_PAIR_OVERWRITE : 0u), pscratch,
+                                                      sb, spost)))
             return rc;
     }
-    if (want_pairs && n_panels == 0) HIPCHK(hipMemsetAsync(pairs, 0, (size_t)n * n * 8, spost));
+    if (r.pairs && n_panels == 0) HIPCHK(hipMemsetAsync(r.pairs, 0, (size_t)n * n * 8, spost));
     HIPCHK(hipEventRecord(I->drawn, sdraw));
     HIPCHK(hipStreamWaitEvent(spost, I->drawn, 0));
-    if (want_unique && (rc = csa_unique_async(hashes, panels, n_panels, W, table, slots, uniq, status, spost)))
+    if (r.uniq && (rc = csa_unique_async(r.hashes, r.panels, n_panels, W, r.table, r.slots, r.uniq, r.status, spost)))
         return rc;
+    return CSA_OK;
+}
+
+int csa_legacy_sample(csa_instance *I, int32_t k, uint64_t seed, uint64_t panel_begin, uint64_t n_panels,
+                      uint32_t flags, uint32_t max_attempts, uint64_t *panels_out, int64_t *person_counts,
+                      int64_t *pair_counts, uint64_t *unique_out, uint32_t *attempts_out) {
+    if (!I) return fail(CSA_E_INVALID, "null instance");
+    if ((flags & CSA_WANT_PANELS) && !panels_out) return fail(CSA_E_INVALID, "panels_out is NULL");
+    if ((flags & CSA_WANT_COUNTS) && !person_counts) return fail(CSA_E_INVALID, "person_counts is NULL");
+    if ((flags & CSA_WANT_PAIRS) && !pair_counts) return fail(CSA_E_INVALID, "pair_counts is NULL");
+    if ((flags & CSA_WANT_UNIQUE) && !unique_out) return fail(CSA_E_INVALID, "unique_out is NULL");
+    int rc = check_quotas(I, k);
+    if (rc) return rc;
+    ScopedDevice sd(I->device);
+    struct Drain {
+        csa_instance *I;
+        ~Drain() { sample_drain(I); }
+    } drain{I};
+    SampleRun r;
+    if ((rc = sample_enqueue(I, k, seed, panel_begin, n_panels, flags, max_attempts, attempts_out != nullptr, true, r)))
+        return rc;
+    const hipStream_t spost = I->spost;
+    const int n = I->n, W = I->W;
     uint32_t hs[4];
-    if ((rc = read_status(status, spost, hs))) return rc;
+    if ((rc = read_status(r.status, spost, hs))) return rc;
     if ((rc = csa_status_decode(hs))) return rc;
     if (flags & CSA_WANT_PANELS)
-        HIPCHK(hipMemcpyAsync(panels_out, panels, n_panels * W * 8, hipMemcpyDeviceToHost, spost));
-    if (want_counts) HIPCHK(hipMemcpyAsync(person_counts, counts, (size_t)n * 8, hipMemcpyDeviceToHost, spost));
-    if (want_pairs) HIPCHK(hipMemcpyAsync(pair_counts, pairs, (size_t)n * n * 8, hipMemcpyDeviceToHost, spost));
-    if (want_unique) HIPCHK(hipMemcpyAsync(unique_out, uniq, 8, hipMemcpyDeviceToHost, spost));
-    if (attempts_out) HIPCHK(hipMemcpyAsync(attempts_out, attempts, n_panels * 4, hipMemcpyDeviceToHost, spost));
+        HIPCHK(hipMemcpyAsync(panels_out, r.panels, n_panels * W * 8, hipMemcpyDeviceToHost, spost));
+    if (flags & CSA_WANT_COUNTS)
+        HIPCHK(hipMemcpyAsync(person_counts, r.counts, (size_t)n * 8, hipMemcpyDeviceToHost, spost));
+    if (flags & CSA_WANT_PAIRS)
+        HIPCHK(hipMemcpyAsync(pair_counts, r.pairs, (size_t)n * n * 8, hipMemcpyDeviceToHost, spost));
+    if (flags & CSA_WANT_UNIQUE) HIPCHK(hipMemcpyAsync(unique_out, r.uniq, 8, hipMemcpyDeviceToHost, spost));
+    if (attempts_out) HIPCHK(hipMemcpyAsync(attempts_out, r.attempts, n_panels * 4, hipMemcpyDeviceToHost, spost));
     HIPCHK(hipStreamSynchronize(spost));
+    return CSA_OK;
+}
+
+// The instance's copy on device `dev` for shard s of csa_legacy_sample_devices (shard 0 on the
+// instance's own device is the instance itself).  A replica mirrors the instance's draw state and
+// address rings as of the last csa_instance_set_state / csa_instance_set_address (generation).
+static int shard_instance(csa_instance *I, int s, int dev, csa_instance **out) {
+    if (s == 0 && dev == I->device) {
+        *out = I;
+        return CSA_OK;
+    }
+    if ((int)I->replicas.size() <= s) {
+        I->replicas.resize(s + 1, nullptr);
+        I->replica_gen.resize(s + 1, 0);
+    }
+    csa_instance *&R = I->replicas[s];
+    if (R && R->device != dev) {
+        csa_instance_destroy(R);
+        R = nullptr;
+    }
+    int rc;
+    if (!R) {
+        ScopedDevice sd(dev);
+        if ((rc = csa_instance_create(I->n, I->C, I->F, I->pf.data(), I->fmin.data(), I->fmax.data(), I->fcat.data(),
+                                      &R)))
+            return rc;
+        I->replica_gen[s] = 0;
+    }
+    if (I->replica_gen[s] != I->gen) {
+        if ((rc = csa_instance_set_state(R, I->sel0.data(), I->rem0h.empty() ? nullptr : I->rem0h.data(),
+                                         I->present0h.empty() ? nullptr : I->present0h.data())) ||
+            (rc = csa_instance_set_address(R, I->addr_h.empty() ? nullptr : I->addr_h.data())))
+            return rc;
+        I->replica_gen[s] = I->gen;
+    }
+    *out = R;
+    return CSA_OK;
+}
+
+// Scratch slots of the multi-device combine (above the batch's own, kSampleSlot0..)
+constexpr int kShardSlot0 = 20, kRootSlot0 = 24;
+
+int csa_legacy_sample_devices(csa_instance *I, const int32_t *devices, int32_t n_shards, int32_t k, uint64_t seed,
+                              uint64_t panel_begin, uint64_t n_panels, uint32_t flags, uint32_t max_attempts,
+                              uint64_t *panels_out, int64_t *person_counts, int64_t *pair_counts,
+                              uint64_t *unique_out, uint32_t *attempts_out) {
+    if (!I) return fail(CSA_E_INVALID, "null instance");
+    if (n_shards <= 0 || n_shards > kMaxWorld) return fail(CSA_E_INVALID, "n_shards must be in [1, %d]", kMaxWorld);
+    if ((flags & CSA_WANT_PANELS) && !panels_out) return fail(CSA_E_INVALID, "panels_out is NULL");
+    if ((flags & CSA_WANT_COUNTS) && !person_counts) return fail(CSA_E_INVALID, "person_counts is NULL");
+    if ((flags & CSA_WANT_PAIRS) && !pair_counts) return fail(CSA_E_INVALID, "pair_counts is NULL");
+    if ((flags & CSA_WANT_UNIQUE) && !unique_out) return fail(CSA_E_INVALID, "unique_out is NULL");
+    int ndev = 0;
+    HIPCHK(hipGetDeviceCount(&ndev));
+    std::vector<int> dev(n_shards);
+    for (int s = 0; s < n_shards; ++s) {
+        dev[s] = devices ? devices[s] : s;
+        if (dev[s] < 0 || dev[s] >= ndev)
+            return fail(CSA_E_INVALID, "shard %d: device %d outside [0, %d)", s, dev[s], ndev);
+    }
+    int rc = check_quotas(I, k);
+    if (rc) return rc;
+    const int n = I->n, W = I->W;
+    std::vector<csa_instance *> R(n_shards, nullptr);
+    for (int s = 0; s < n_shards; ++s)
+        if ((rc = shard_instance(I, s, dev[s], &R[s]))) return rc;
+    struct DrainAll {
+        std::vector<csa_instance *> &R;
+        ~DrainAll() {
+            for (csa_instance *x : R)
+                if (x) sample_drain(x);
+        }
+    } drain{R};
+    // 1. every shard draws, counts and pairs its contiguous panel range and reduces it to its exact
+    //    local distinct panels (csa_exchange_pack_async with one owner), all enqueued before any wait
+    const bool want_unique = flags & CSA_WANT_UNIQUE, want_pairs = flags & CSA_WANT_PAIRS;
+    const bool want_counts = flags & CSA_WANT_COUNTS;
+    const uint32_t sflags = flags & (CSA_WANT_COUNTS | CSA_WANT_PAIRS | CSA_WANT_UNIQUE);
+    std::vector<uint64_t> b(n_shards + 1);
+    for (int s = 0; s <= n_shards; ++s) b[s] = n_panels * (uint64_t)s / (uint64_t)n_shards;
+    uint64_t cap = 1;
+    for (int s = 0; s < n_shards; ++s) cap = std::max(cap, b[s + 1] - b[s]);
+    std::vector<SampleRun> run(n_shards);
+    std::vector<uint64_t *> sh(n_shards, nullptr), sp(n_shards, nullptr), sc(n_shards, nullptr);
+    for (int s = 0; s < n_shards; ++s) {
+        csa_instance *X = R[s];
+        ScopedDevice sd(X->device);
+        const uint64_t len = b[s + 1] - b[s];
+        if ((rc = sample_enqueue(X, k, seed, panel_begin + b[s], len, sflags, max_attempts, attempts_out != nullptr,
+                                 false, run[s])))
+            return rc;
+        if (!want_unique) continue;
+        const uint64_t xb = csa_exchange_scratch_bytes(len);
+        void *xs = nullptr;
+        if ((rc = scratch(X, kShardSlot0, 2 * cap, &sh[s])) || (rc = scratch(X, kShardSlot0 + 1, cap * W, &sp[s])) ||
+            (rc = scratch(X, kShardSlot0 + 2, 1, &sc[s])) ||
+            (rc = scratch(X, kShardSlot0 + 3, xb, reinterpret_cast<uint8_t **>(&xs))))
+            return rc;
+        if ((rc = csa_exchange_pack_async(run[s].hashes, run[s].panels, len, W, 1, cap, xs, xb, sh[s], sp[s], sc[s],
+                                          run[s].status, X->spost)))
+            return rc;
+    }
+    // 2. every shard's status, its panels / attempts straight into the caller's buffers
+    for (int s = 0; s < n_shards; ++s) {
+        csa_instance *X = R[s];
+        ScopedDevice sd(X->device);
+        const uint64_t len = b[s + 1] - b[s];
+        uint32_t hs[4];
+        if ((rc = read_status(run[s].status, X->spost, hs))) return rc;
+        if ((rc = csa_status_decode(hs))) return rc;
+        if ((flags & CSA_WANT_PANELS) && len)
+            HIPCHK(hipMemcpyAsync(panels_out + b[s] * W, run[s].panels, len * W * 8, hipMemcpyDeviceToHost, X->spost));
+        if (attempts_out && len)
+            HIPCHK(hipMemcpyAsync(attempts_out + b[s], run[s].attempts, len * 4, hipMemcpyDeviceToHost, X->spost));
+    }
+    // 3. combine on shard 0's device: counts and pairs summed (peer copies over xGMI + one add
+    //    kernel per shard), the local distinct sets gathered as segments and counted exactly
+    //    (hash AND bitmask) by csa_unique_segments_async
+    csa_instance *X0 = R[0];
+    ScopedDevice sd0(X0->device);
+    const hipStream_t st = X0->spost;
+    const size_t nn = want_pairs ? (size_t)n * n : 0, nc = (want_counts || want_pairs) ? (size_t)n : 0;
+    int64_t *tmp = nullptr;
+    if (n_shards > 1 && nc && (rc = scratch(X0, kRootSlot0, nc + nn, &tmp))) return rc;
+    uint64_t *gh = nullptr, *gp = nullptr, *gc = nullptr, *table = nullptr, *uniq = nullptr;
+    const uint64_t total = (uint64_t)n_shards * cap, slots = pow2_at_least(std::max<uint64_t>(2 * total, 64));
+    if (want_unique &&
+        ((rc = scratch(X0, kRootSlot0 + 1, 2 * total, &gh)) || (rc = scratch(X0, kRootSlot0 + 2, total * W, &gp)) ||
+         (rc = scratch(X0, kRootSlot0 + 3, (size_t)n_shards, &gc)) || (rc = scratch(X0, kRootSlot0 + 4, slots, &table)) ||
+         (rc = scratch(X0, kRootSlot0 + 5, 1, &uniq))))
+        return rc;
+    for (int s = 0; s < n_shards; ++s) {
+        const int d = R[s]->device;
+        if (s > 0 && nc) {
+            HIPCHK(hipMemcpyPeerAsync(tmp, X0->device, run[s].counts, d, nc * 8, st));
+            if (nn) HIPCHK(hipMemcpyPeerAsync(tmp + nc, X0->device, run[s].pairs, d, nn * 8, st));
+            // counts and pairs are adjacent in tmp but not in the shard-0 buffers: two adds
+            hipLaunchKernelGGL(add_i64_kernel, dim3((unsigned)((nc + 255) / 256)), dim3(256), 0, st, run[0].counts,
+                               (const int64_t *)tmp, (uint64_t)nc);
+            if (nn)
+                hipLaunchKernelGGL(add_i64_kernel, dim3((unsigned)std::min<uint64_t>((nn + 255) / 256, 65536)), dim3(256),
+                                   0, st, run[0].pairs, (const int64_t *)(tmp + nc), (uint64_t)nn);
+            HIPCHK(hipGetLastError());
+        }
+        if (want_unique) {
+            HIPCHK(hipMemcpyPeerAsync(gh + 2 * cap * s, X0->device, sh[s], d, 2 * cap * 8, st));
+            HIPCHK(hipMemcpyPeerAsync(gp + cap * W * s, X0->device, sp[s], d, cap * W * 8, st));
+            HIPCHK(hipMemcpyPeerAsync(gc + s, X0->device, sc[s], d, 8, st));
+        }
+    }
+    if (want_unique) {
+        HIPCHK(hipMemsetAsync(uniq, 0, 8, st));
+        if ((rc = csa_unique_segments_async(gh, gp, (uint32_t)n_shards, cap, gc, W, table, slots, uniq, run[0].status,
+                                            st)))
+            return rc;
+    }
+    uint32_t hs[4];
+    if ((rc = read_status(run[0].status, st, hs))) return rc;
+    if ((rc = csa_status_decode(hs))) return rc;
+    if (want_counts) HIPCHK(hipMemcpyAsync(person_counts, run[0].counts, (size_t)n * 8, hipMemcpyDeviceToHost, st));
+    if (want_pairs) HIPCHK(hipMemcpyAsync(pair_counts, run[0].pairs, nn * 8, hipMemcpyDeviceToHost, st));
+    if (want_unique) HIPCHK(hipMemcpyAsync(unique_out, uniq, 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
     return CSA_OK;
 }
 

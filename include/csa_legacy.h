@@ -14,8 +14,9 @@
  *     the ABI; every function returns a CSA_* status code (0 = ok) and leaves
  *     a thread-local message in csa_last_error().
  *   - an instance lives on the HIP device that was current when it was
- *     created (one process per GPU; multi-GPU sharding and the RCCL
- *     all-reduce live in the Python layer, see DESIGN.md "Multi-GPU").
+ *     created.  Multi-GPU: one process per GPU with the RCCL exchange in the
+ *     Python layer (DESIGN.md "Multi-GPU"), or several devices of one process
+ *     through csa_legacy_sample_devices (replicas owned by the handle).
  *   - agent ids are 0..n-1 = pool row order (analysis.py:131-133); feature
  *     ids are 0..F-1 in category-major CSV order (analysis.py:114-124).
  *   - randomness: Philox4x32-10 verification-mode stream, keyed by
@@ -99,6 +100,21 @@ int csa_legacy_sample(csa_instance *inst, int32_t k, uint64_t seed, uint64_t pan
                       uint64_t n_panels, uint32_t flags, uint32_t max_attempts,
                       uint64_t *panels_out, int64_t *person_counts, int64_t *pair_counts,
                       uint64_t *unique_out, uint32_t *attempts_out);
+
+/* legacy_probabilities (analysis.py:162-191) over several devices of this process: the n_devices
+ * argument of SURVEY.md §8(b)'s proposed csa_legacy_sample, for callers without torch.distributed.
+ * Shard s (0 <= s < n_shards) draws the contiguous panel range
+ *   [panel_begin + n_panels*s/n_shards, panel_begin + n_panels*(s+1)/n_shards)
+ * on device devices[s] (NULL: device s; a device may repeat), on a replica of the instance that
+ * the handle owns and keeps across calls (it mirrors csa_instance_set_state / _set_address).
+ * Per-person and pair counts are summed on shard 0's device (peer copies + an add kernel); every
+ * shard reduces its panels to its exact local distinct set and shard 0 counts the union exactly
+ * (128-bit hash AND W-word bitmask).  Results are identical to csa_legacy_sample over the same
+ * range for any n_shards and device list.  Arguments and outputs as csa_legacy_sample. */
+int csa_legacy_sample_devices(csa_instance *inst, const int32_t *devices, int32_t n_shards, int32_t k,
+                              uint64_t seed, uint64_t panel_begin, uint64_t n_panels, uint32_t flags,
+                              uint32_t max_attempts, uint64_t *panels_out, int64_t *person_counts,
+                              int64_t *pair_counts, uint64_t *unique_out, uint32_t *attempts_out);
 
 /* legacy_find (analysis.py:141-159), batched: panels in pick order.
  * picks_out: n_panels * k int32 (a step that picked nobody -- only possible
