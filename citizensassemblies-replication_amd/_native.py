@@ -114,6 +114,8 @@ def lib():
     except OSError as e:
         raise NativeLibraryError("failed to load %s: %s" % (LIB_PATH, e)) from e
     for name, (res, args) in SIGNATURES.items():
+        if os.environ.get("CSA_LIB") and not hasattr(L, name):
+            continue  # an older A/B build (CSA_LIB) may predate newer entry points
         fn = getattr(L, name)
         fn.restype = res
         fn.argtypes = args

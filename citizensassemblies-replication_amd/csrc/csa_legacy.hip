@@ -560,6 +560,7 @@ __global__ __launch_bounds__(draw_threads(FPL, WPL), draw_occupancy(FPL, WPL)) v
 
 #include "draw_lane.inc"
 #include "draw_wide.inc"
+#include "draw_solo.inc"
 
 // 128-bit panel hashes (the draw_kernel's in-kernel hash, for the batch kernel's panels): a
 // quad of lanes per panel, words glane, glane+4, ... (coalesced within the quad), quad sum.
@@ -1296,8 +1297,9 @@ struct DrawConfig {
     int G = 16, FPL = 1, WPL = 1;
     bool lane = false;  // draw_lane_kernel (2 lanes per panel): FPL / WPL hold its FN / WN
     bool wide = false;  // draw_wide_kernel (8 lanes per panel)
+    bool solo = false;  // draw_solo_kernel (1 lane per panel): FPL / WPL hold its FN / WN
     const void *fn = nullptr;
-    bool picks() const { return lane || wide; }  // pick-list kernels (picks_pack_kernel builds the panels)
+    bool picks() const { return lane || wide || solo; }  // pick-list kernels (picks_pack_kernel builds the panels)
 };
 
 template <int FPL>
@@ -1339,6 +1341,27 @@ const void *lane_fn_w(int wn) {
         case 16: return lane_fn_wn<FN, 16>();
         case 28: return lane_fn_wn<FN, 28>();
         case 32: return lane_fn_wn<FN, 32>();
+        default: return nullptr;
+    }
+}
+
+template <int FN>
+const void *solo_fn_w(int wn) {
+    switch (wn) {
+        case 4: return reinterpret_cast<const void *>(&draw_solo_kernel<FN, 4>);
+        case 8: return reinterpret_cast<const void *>(&draw_solo_kernel<FN, 8>);
+        case 16: return reinterpret_cast<const void *>(&draw_solo_kernel<FN, 16>);
+        case 28: return reinterpret_cast<const void *>(&draw_solo_kernel<FN, 28>);
+        case 32: return reinterpret_cast<const void *>(&draw_solo_kernel<FN, 32>);
+        default: return nullptr;
+    }
+}
+
+const void *solo_fn(int fn_, int wn) {
+    switch (fn_) {
+        case 8: return solo_fn_w<8>(wn);
+        case 16: return solo_fn_w<16>(wn);
+        case 32: return solo_fn_w<32>(wn);
         default: return nullptr;
     }
 }
@@ -1399,12 +1422,21 @@ int pick_draw_config(const csa_instance *I, bool general, DrawConfig &c) {
     const bool g16_ok = I->F <= 64 && I->W <= 256;
     int choice = general ? 64 : lane_ok ? 2 : wide_ok ? 8 : g16_ok ? 16 : 64;
     if (const char *e = getenv("CSA_DRAW_KERNEL")) {
-        if (!general && !strcmp(e, "lane") && lane_ok) choice = 2;
+        if (!general && !strcmp(e, "solo") && lane_ok) choice = 1;
+        else if (!general && !strcmp(e, "lane") && lane_ok) choice = 2;
         else if (!general && !strcmp(e, "wide") && wide_ok) choice = 8;
         else if (!general && !strcmp(e, "16") && g16_ok) choice = 16;
         else if (!general && !strcmp(e, "64")) choice = 64;
     }
     c.G = choice;
+    if (choice == 1) {
+        c.solo = true;
+        c.FPL = std::max(8, pow2_ceil_int(I->F));
+        c.WPL = I->W <= 4 ? 4 : I->W <= 8 ? 8 : I->W <= 16 ? 16 : I->W <= 28 ? 28 : 32;
+        c.fn = solo_fn(c.FPL, c.WPL);
+        if (!c.fn) return fail(CSA_E_UNSUPPORTED, "no solo draw kernel for F=%d W=%d", I->F, I->W);
+        return CSA_OK;
+    }
     if (choice == 8) {  // draw_wide_kernel: FPL in {2, 4, 5, 8}, WPL in {4, 8, 16}
         const int fpl = (I->F + 7) / 8;
         c.wide = true;
@@ -1555,9 +1587,13 @@ int launch_draw(const csa_instance *I, int32_t k, uint64_t seed, uint64_t panel_
         A.picks16 = d_picks_ext;
     else if (cfg.picks() && (rc = lane_picks(M, n_panels * (uint64_t)((k + 7) & ~7), stream, &A.picks16)))
         return rc;
-    const int threads = cfg.lane ? kLaneThreads : cfg.wide ? kWideThreads : draw_threads(cfg.FPL, cfg.WPL);
+    const int threads = cfg.lane   ? kLaneThreads
+                        : cfg.solo ? kSoloThreads
+                        : cfg.wide ? kWideThreads
+                                   : draw_threads(cfg.FPL, cfg.WPL);
     const int groups_wg = threads / cfg.G;
     const size_t lds = cfg.lane   ? lane_lds_bytes(cfg.FPL, cfg.WPL, I->n)
+                       : cfg.solo ? solo_lds_bytes(cfg.FPL, cfg.WPL, I->n)
                        : cfg.wide ? wide_lds_bytes(cfg.G, cfg.FPL, cfg.WPL)
                                   : draw_lds_bytes(cfg.G, cfg.FPL, cfg.WPL, I->W, k, groups_wg);
     if (lds > 160 * 1024) return fail(CSA_E_UNSUPPORTED, "draw kernel needs %zu B of LDS", lds);
@@ -1574,8 +1610,8 @@ int launch_draw(const csa_instance *I, int32_t k, uint64_t seed, uint64_t panel_
     }
     // the lane kernel packs its own panels (one workgroup per 128 panels, so every workgroup knows
     // its panel range); the wide kernel's pick lists are packed by picks_pack_kernel
-    const bool fused = cfg.lane && !d_picks_ext && d_panels;
-    if (cfg.lane && !fused) {
+    const bool fused = (cfg.lane || cfg.solo) && !d_picks_ext && d_panels;
+    if ((cfg.lane || cfg.solo) && !fused) {
         A.panels = nullptr;
         A.hashes = nullptr;
     }
@@ -2005,7 +2041,9 @@ int csa_draw_kernel_name(const csa_instance *I, int32_t k, char *buf, uint64_t l
     DrawConfig cfg;
     rc = pick_draw_config(I, false, cfg);
     if (rc) return rc;
-    if (cfg.lane)
+    if (cfg.solo)
+        snprintf(buf, (size_t)len, "draw_solo_kernel<%d, %d>", cfg.FPL, cfg.WPL);
+    else if (cfg.lane)
         snprintf(buf, (size_t)len, "draw_lane_kernel<%d, %d, %d>", cfg.FPL, cfg.WPL,
                  (cfg.WPL / 2 + CSA_LANE_SKDIV - 1) / CSA_LANE_SKDIV);
     else if (cfg.wide)

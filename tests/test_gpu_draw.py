@@ -1,9 +1,9 @@
 """GPU parity of every draw-kernel layout against the C oracle (Philox verification mode).
 
-The batch path picks draw_lane_kernel (2 lanes per panel) or draw_wide_kernel (8 lanes per
-panel, n up to 8192), both writing pick lists that picks_pack_kernel packs, or draw_kernel
-(G = 16 / 64) from the instance shape; CSA_DRAW_KERNEL=lane|wide|16|64 forces a layout the
-instance fits.  Each must give the
+The batch path picks draw_solo_kernel (1 lane per panel), draw_lane_kernel (2 lanes per
+panel) or draw_wide_kernel (8 lanes per panel, n up to 8192), all writing pick lists (packed
+in the draw's tail or by picks_pack_kernel), or draw_kernel (G = 16 / 64) from the instance
+shape; CSA_DRAW_KERNEL=solo|lane|wide|16|64 forces a layout the instance fits.  Each must give the
 oracle's panels and attempt counts bit-exactly, including the edge cases of
 legacy.py:124-200 (restarts, rejections, max = 0 features, max = 0 < min).
 """
@@ -12,7 +12,7 @@ import os
 import numpy as np
 import pytest
 
-from conftest import inst_paths, pkg
+from conftest import PHILOX_CASES, golden, inst_paths, pkg
 from oracle import coracle
 from oracle.legacy_oracle import OracleInstance, read_instance as oracle_read
 
@@ -21,7 +21,7 @@ pytestmark = pytest.mark.gpu
 
 @pytest.fixture
 def draw_group():
-    """Force a batch draw layout (CSA_DRAW_KERNEL = "lane" / "wide" / "16" / "64")."""
+    """Force a batch draw layout (CSA_DRAW_KERNEL = "solo" / "lane" / "wide" / "16" / "64")."""
     old = os.environ.get("CSA_DRAW_KERNEL")
 
     def set_layout(g):
@@ -42,7 +42,7 @@ def _sample(enc, k, S, seed, begin=0, max_attempts=0):
     return panels, attempts
 
 
-@pytest.mark.parametrize("group", ["lane", "wide", 16, 64])
+@pytest.mark.parametrize("group", ["solo", "lane", "wide", 16, 64])
 @pytest.mark.parametrize("name,k,S,seed", [("sf_e_tight_110", 110, 3000, 5), ("pathological_5", 5, 4000, 2),
                                            ("rejecty_6", 6, 20000, 8), ("example_small_20", 20, 20000, 1),
                                            ("couples_panel_from_twenty_people_no_constraints_2", 2, 20000, 3),
@@ -71,7 +71,7 @@ def _weird_instance():
     return cats, agents
 
 
-@pytest.mark.parametrize("group", ["lane", "wide", 16, 64])
+@pytest.mark.parametrize("group", ["solo", "lane", "wide", 16, 64])
 def test_zero_max_features_match_oracle(gpu_available, draw_group, group):
     """max = 0 features (dead, and max = 0 < min which routes to draw_kernel) vs the oracle."""
     P = pkg()
@@ -167,3 +167,21 @@ def test_k_zero_draws_empty_panels(gpu_available):
     enc = P.encode(cats, agents)
     with pytest.raises(N.CsaError):
         _sample(enc, 0, 10, 3, max_attempts=5)
+
+
+@pytest.mark.parametrize("group", ["solo", "lane"])
+@pytest.mark.parametrize("case", PHILOX_CASES)
+def test_register_layouts_match_goldens(gpu_available, draw_group, group, case):
+    """The one- and two-lane register kernels (fused pack included) against the reference goldens."""
+    import hashlib
+    P = pkg()
+    A = pkg("analysis")
+    draw_group(group)
+    g = golden(case)
+    inst = P.read_instance(*inst_paths(g["instance"]), g["k"])
+    enc = P.encode(inst.categories, inst.agents)
+    raw = A.legacy_sample_raw(enc, g["k"], g["S"], g["seed"], want_pairs=False, want_panels=True,
+                              want_attempts=True)
+    assert hashlib.sha256(np.ascontiguousarray(raw.panels).tobytes()).hexdigest() == g["panels_sha256"]
+    assert raw.attempts.tolist() == g["attempts"]
+    assert raw.unique == g["unique"]
