@@ -1408,11 +1408,11 @@ int pow2_ceil_int(int x) {
     return p;
 }
 
-// Batch draws: draw_lane_kernel (2 lanes per panel, 32 panels per wavefront) when the instance
-// fits -- F <= 32, W <= 32, no max = 0 < min feature, |min|, |selected| < 2^15 (16-bit packed
+// Batch draws: draw_solo_kernel (1 lane per panel) or draw_lane_kernel (2 lanes per panel, 32
+// panels per wavefront) when the instance fits -- F <= 32, W <= 32, no max = 0 < min feature, |min|, |selected| < 2^15 (16-bit packed
 // need / remaining) and no feature starting above max ("selected == max" is tested as
 // need <= min - max) -- else draw_kernel with G = 16 (F <= 64, W <= 256) or 64.  Pick-order /
-// single-attempt draws (general mode) use draw_kernel<64, ..., true>.  CSA_DRAW_KERNEL=lane|16|64
+// single-attempt draws (general mode) use draw_kernel<64, ..., true>.  CSA_DRAW_KERNEL=solo|lane|wide|16|64
 // forces a batch kernel the instance fits (parity tests of every layout).
 int pick_draw_config(const csa_instance *I, bool general, DrawConfig &c) {
     general = general || I->d_addr_next;  // same-address deletions: draw_kernel<64, ..., true> only
@@ -1420,7 +1420,11 @@ int pick_draw_config(const csa_instance *I, bool general, DrawConfig &c) {
                          !I->sel_over_max && I->max_slack <= 255;
     const bool wide_ok = I->F <= 64 && I->W <= 128 && !I->zero_max_min && I->max_abs < 32768 && !I->sel_over_max;
     const bool g16_ok = I->F <= 64 && I->W <= 256;
-    int choice = general ? 64 : lane_ok ? 2 : wide_ok ? 8 : g16_ok ? 16 : 64;
+    // one lane per panel when a lane holds few features (F <= 16: 142 VGPRs at W = 32, 3 waves/SIMD;
+    // example_large_200 281 vs 252 M panels/s, example_small_20 2950 vs 2490); at F = 32 the state needs
+    // 165 VGPRs and the two-lane kernel's 4 waves/SIMD win (sf_e 262 vs 247)
+    const bool solo_ok = lane_ok && I->F <= 16;
+    int choice = general ? 64 : solo_ok ? 1 : lane_ok ? 2 : wide_ok ? 8 : g16_ok ? 16 : 64;
     if (const char *e = getenv("CSA_DRAW_KERNEL")) {
         if (!general && !strcmp(e, "solo") && lane_ok) choice = 1;
         else if (!general && !strcmp(e, "lane") && lane_ok) choice = 2;
