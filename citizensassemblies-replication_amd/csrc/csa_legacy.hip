@@ -1361,15 +1361,12 @@ const void *solo_fn(int fn_, int wn) {
     switch (fn_) {
         case 8: return solo_fn_w<8>(wn);
         case 16: return solo_fn_w<16>(wn);
-        case 32: return solo_fn_w<32>(wn);
         default: return nullptr;
     }
 }
 
 const void *lane_fn(int fn_, int wn) {
     switch (fn_) {
-        case 8: return lane_fn_w<8>(wn);
-        case 16: return lane_fn_w<16>(wn);
         case 32: return lane_fn_w<32>(wn);
         default: return nullptr;
     }
@@ -1426,8 +1423,9 @@ int pick_draw_config(const csa_instance *I, bool general, DrawConfig &c) {
     const bool solo_ok = lane_ok && I->F <= 16;
     int choice = general ? 64 : solo_ok ? 1 : lane_ok ? 2 : wide_ok ? 8 : g16_ok ? 16 : 64;
     if (const char *e = getenv("CSA_DRAW_KERNEL")) {
-        if (!general && !strcmp(e, "solo") && lane_ok) choice = 1;
-        else if (!general && !strcmp(e, "lane") && lane_ok) choice = 2;
+        // the register kernels are built for the shapes they win on only (solo F <= 16, lane F > 16)
+        if (!general && !strcmp(e, "solo") && solo_ok) choice = 1;
+        else if (!general && !strcmp(e, "lane") && lane_ok && !solo_ok) choice = 2;
         else if (!general && !strcmp(e, "wide") && wide_ok) choice = 8;
         else if (!general && !strcmp(e, "16") && g16_ok) choice = 16;
         else if (!general && !strcmp(e, "64")) choice = 64;
