@@ -608,10 +608,11 @@ __device__ __forceinline__ uint64_t wave_transpose64(uint64_t x, int lane) {
     return x;
 }
 
-// blockIdx.y = column range: words [CW y, CW y + CW) of every panel, i.e. agents [64 CW y, ...) --
-// one range for n <= 64 kXtCols agents, two for n up to 16384 (the tile and the counts of a range
-// fit the LDS)
-constexpr int kXtCols = 128;
+// blockIdx.y = column range: words [CW y, CW y + CW) of every panel, i.e. agents [64 CW y, ...).
+// 32 words per range: a 17 KB tile + 8 KB of counts per workgroup, so ~6 workgroups share a CU and
+// one's loads overlap another's transposes (128-word ranges at n = 8192 needed 98 KB, one
+// workgroup per CU, and moved 2 GB per 10^6 panels at 0.9 TB/s)
+constexpr int kXtCols = 32;
 __global__ __launch_bounds__(kXtThreads) void xt_count_kernel(const uint64_t *__restrict__ panels,
                                                               uint64_t S, int n, int W, int npad,
                                                               uint64_t *__restrict__ xt,
@@ -778,6 +779,8 @@ __global__ __launch_bounds__(kPairThreads) void pair_mfma_kernel(const uint64_t 
                 const uint64_t *w = words[buf][j];
                 if constexpr (FP4) {
                     // lane half h needs only the 32-bit half h of each word: read it directly
+                    // (a split into two 32-bit planes, conflict-free for these reads, measured
+                    // 1-5 % slower: twice the staging stores)
                     const uint32_t *w32 = reinterpret_cast<const uint32_t *>(w) + h;
                     v8i fa[4], fb[2];
 #pragma unroll
