@@ -185,3 +185,51 @@ def test_register_layouts_match_goldens(gpu_available, draw_group, group, case):
     assert hashlib.sha256(np.ascontiguousarray(raw.panels).tobytes()).hexdigest() == g["panels_sha256"]
     assert raw.attempts.tolist() == g["attempts"]
     assert raw.unique == g["unique"]
+
+
+def _synthetic(F_per_cat, n, k, seed):
+    """Random pool: categories with the given feature counts, shares ~ Dirichlet(2), quotas
+    floor(0.9 k p) / ceil(1.1 k p) (the SURVEY §8(d) synthetic recipe)."""
+    rng = np.random.default_rng(seed)
+    cats, feats, fmin, fmax, fcat = {}, [], [], [], []
+    shares = []
+    for c, nf in enumerate(F_per_cat):
+        p = rng.dirichlet(np.full(nf, 2.0))
+        shares.append(p)
+        cats["c%d" % c] = {}
+        for j in range(nf):
+            lo, hi = int(np.floor(0.9 * k * p[j])), int(np.ceil(1.1 * k * p[j]))
+            cats["c%d" % c]["f%d" % j] = {"min": lo, "max": hi}
+            feats.append(("c%d" % c, "f%d" % j))
+            fmin.append(lo)
+            fmax.append(hi)
+            fcat.append(c)
+    picks = [rng.choice(len(p), size=n, p=p) for p in shares]
+    agents = {i: {"c%d" % c: "f%d" % picks[c][i] for c in range(len(F_per_cat))} for i in range(n)}
+    pf = [[feats.index(("c%d" % c, "f%d" % picks[c][i])) for c in range(len(F_per_cat))] for i in range(n)]
+    o = OracleInstance(k=k, cat_names=list(cats), feat_names=feats, fmin=fmin, fmax=fmax, fcat=fcat,
+                       person_feat=pf)
+    return cats, agents, o
+
+
+@pytest.mark.parametrize("F_per_cat,n,k", [((4, 4, 4), 1800, 100),   # one-lane kernel FN = 16, WN = 32
+                                           ((4, 4, 4), 1700, 100),   # FN = 16, WN = 28: 4 recount parts of 7 words
+                                           ((3, 3), 1700, 120),      # FN = 8, WN = 28: 4 parts
+                                           ((3, 3), 200, 30),        # FN = 8, WN = 4
+                                           ((5, 5, 4), 100, 20)])    # FN = 16, WN = 4: one word per part
+def test_one_lane_layouts_match_oracle(gpu_available, F_per_cat, n, k):
+    """draw_solo_kernel's recount layouts (64/FN word parts, fewer where they do not divide WN)
+    on synthetic pools the public instances do not cover, against the C oracle."""
+    P = pkg()
+    N = pkg("_native")
+    cats, agents, o = _synthetic(F_per_cat, n, k, seed=n + k)
+    enc = P.encode(cats, agents)
+    buf = np.zeros(64, np.uint8)
+    N.check(N.lib().csa_draw_kernel_name(enc.handle, k, buf.ctypes.data_as(__import__("ctypes").c_char_p), 64))
+    assert bytes(buf).split(b"\0")[0].startswith(b"draw_solo_kernel")
+    S, seed, begin = 4000, 3, 77
+    rc, opanels, oatt, _ = coracle.draw(o, k, seed, begin, S, max_attempts=100000)
+    panels, attempts = _sample(enc, k, S, seed, begin)
+    assert rc == 0
+    assert np.array_equal(attempts, oatt)
+    assert np.array_equal(panels, opanels)
