@@ -4,11 +4,12 @@
 set -u
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}; OUT=$ROOT/gpurun_out; mkdir -p "$OUT"; cd "$ROOT"
 P=${1:-200000}
-timeout -k 10 300 python bench.py --steps 20 --warmup 2 --no-cpu-baseline --no-api --panels $((2 * P)) > "$OUT/reh_n1.json" 2> "$OUT/reh_n1.err"
+CFG=${2:-sf_e_110}
+timeout -k 10 300 python bench.py --config $CFG --steps 20 --warmup 2 --no-cpu-baseline --no-api --panels $((2 * P)) > "$OUT/reh_n1.json" 2> "$OUT/reh_n1.err"
 rc=$?; echo "[n1] rc=$rc"; [ $rc -eq 0 ] || { tail -5 "$OUT/reh_n1.err"; exit $rc; }
 CSA_BENCH_BACKEND=gloo timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
-    --master-addr 127.0.0.1 --master-port 29531 bench.py --gpus 2 --steps 20 --warmup 2 --no-cpu-baseline --no-api \
-    --panels $P > "$OUT/reh_n2.json" 2> "$OUT/reh_n2.err"
+    --master-addr 127.0.0.1 --master-port 29531 bench.py --config $CFG --gpus 2 --steps 20 --warmup 2 --no-cpu-baseline \
+    --no-api --panels $P > "$OUT/reh_n2.json" 2> "$OUT/reh_n2.err"
 rc=$?; echo "[n2] rc=$rc"; [ $rc -eq 0 ] || { tail -20 "$OUT/reh_n2.err"; exit $rc; }
 python3 - "$OUT/reh_n1.json" "$OUT/reh_n2.json" <<'PY'
 import json, sys
