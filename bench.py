@@ -239,16 +239,37 @@ def api_leg(P, A, inst, S, seed):
                                           "copied and divided on first access (pair_histogram_materialise_ms)"}
 
 
+def self_launch(n, script=None, argv=None):
+    """`python bench.py --gpus N` without a launcher: start N rank processes of this same command
+    (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set, one GPU each) and return the worst exit code.
+    Runs before anything imports torch or touches a device in this process."""
+    import socket
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, script or os.path.abspath(__file__)] +
+                                      list(sys.argv[1:] if argv is None else argv), env=env))
+    rcs = [p.wait() for p in procs]
+    bad = [rc for rc in rcs if rc]
+    return max(bad, key=abs) if bad else 0
+
+
 def main():
     args = parse()
-    import torch
-    import torch.distributed as dist
-
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(self_launch(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus and rank == 0:
-        print("warning: --gpus %d but WORLD_SIZE %d" % (args.gpus, world), file=sys.stderr)
+    if world != args.gpus:
+        sys.exit("bench.py: --gpus %d but WORLD_SIZE=%d (launch with matching --nproc-per-node, or without a "
+                 "launcher: bench.py starts --gpus ranks itself)" % (args.gpus, world))
+    import torch
+    import torch.distributed as dist
     # one process per GPU; the modulo only matters for CSA_BENCH_BACKEND=gloo rehearsals of the
     # N > 1 path with several ranks on a 1-GPU box (RCCL refuses two ranks on one device)
     dev_index = local_rank % max(torch.cuda.device_count(), 1)
@@ -384,6 +405,7 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    A.draw_stats(enc, reset=True)     # SelectionErrors / rejections of the timed draws only
     log = {}
     t0 = time.perf_counter()
     run_steps(args.warmup, args.steps, log)
@@ -402,6 +424,32 @@ def main():
     # single-GPU run with --panels N*P (same global panel indices)
     checks = {"last_step_unique": int(last["unique"].item()), "last_step_count_sum": int(pipe.counts.sum().item()),
               "last_step_pair_sum": int(torch.triu(pipe.pairs.view(enc.n, enc.n)).sum().item()) if want_pairs else None}
+    # draw statistics of the timed steps, summed over ranks
+    st = torch.tensor(list(A.draw_stats(enc).values()), dtype=torch.int64, device=dev)
+    if world > 1:
+        Dd._all_reduce(st)
+    draw_stats = dict(zip(A.STAT_KEYS, (int(x) for x in st.cpu().tolist())))
+    draw_stats["panels"] = S * world * args.steps
+    if world > 1:
+        # the one-process multi-device path over the same N GPUs (csa_legacy_sample_devices: a replica
+        # of the instance per device, peer copies + adds on device 0, exact union of the local distinct
+        # sets) for the last timed step's global panel range must equal the rank-sharded result
+        dist.barrier()
+        if rank == 0:
+            j = args.warmup + args.steps - 1
+            ndev = max(torch.cuda.device_count(), 1)
+            devs = [(dev_index + s_) % ndev for s_ in range(world)]
+            raw = A.legacy_sample_raw(enc, k, S * world, args.seed, panel_begin=j * world * S, want_pairs=want_pairs,
+                                      want_panels=False, devices=devs)
+            got_c = pipe.counts.cpu().numpy()
+            same = bool((raw.counts == got_c).all()) and raw.unique == checks["last_step_unique"]
+            if want_pairs:
+                import numpy as np
+                got_p = pipe.pairs.view(enc.n, enc.n).cpu().numpy()
+                same = same and bool(np.array_equal(np.triu(raw.pairs), np.triu(got_p)))
+            checks["sample_devices"] = {"devices": devs, "panels": S * world, "unique": raw.unique,
+                                        "equal_to_rank_sharded": same}
+        dist.barrier()
 
     def stage_times(rec):
         out = {s: 0.0 for s in stages}
@@ -541,6 +589,7 @@ def main():
         "kernels": kernels,
         "kernel_timing": kernel_timing,
         "checks": checks,
+        "draw_stats": draw_stats,
         "draw_stream_busy": draw_busy,
     }
     if want_pairs:

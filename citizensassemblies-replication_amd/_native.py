@@ -73,8 +73,9 @@ SIGNATURES = {
     "csa_pairs_unpack_async": (ctypes.c_int, [_P, _I32, _P, _P]),
     "csa_status_decode": (ctypes.c_int, [_P]),
     "csa_legacy_draw_mt": (ctypes.c_int, [_I32, _I32, _I32, _P, _P, _P, _P, _P, _P, _P, _I32, _P, _U64, _U32,
-                                          _I32, _P, _P, _P, _P, _P, _P]),
+                                          _I32, _P, _P, _P, _P, _P, _P, _P]),
     "csa_instance_set_address": (ctypes.c_int, [_P, _P]),
+    "csa_instance_draw_stats": (ctypes.c_int, [_P, _I32, _P]),
 }
 
 _lib = None

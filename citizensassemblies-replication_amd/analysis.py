@@ -152,10 +152,12 @@ class PanelSet:
     def __len__(self):
         return self._count
 
+    _where = "panels were not kept; only len() is available"
+
     def _materialise(self):
         if self._set is None:
             if self._packed is None:
-                raise RuntimeError("panels were not kept; only len() is available")
+                raise RuntimeError(self._where)
             p = self._packed
             if hasattr(p, "device") and not isinstance(p, np.ndarray):
                 W = (self._n + 63) // 64
@@ -174,6 +176,42 @@ class PanelSet:
 
     def __eq__(self, other):
         return set(self) == set(other)
+
+    def rows(self):
+        """The distinct panels as a host uint64[u, W] array (sorted rows), or None when the panels
+        were not kept.  Device panels are copied to the host here."""
+        W = (self._n + 63) // 64
+        if self._packed is None:
+            if self._set is None:
+                return None
+            pos = {aid: q for q, aid in enumerate(self._ids)}
+            rows = np.zeros((len(self._set), max(W, 1)), np.uint64)
+            for i, panel in enumerate(self._set):
+                for aid in panel:
+                    q = pos[aid]
+                    rows[i, q >> 6] |= np.uint64(1) << np.uint64(q & 63)
+            return np.unique(rows, axis=0) if len(rows) else rows
+        p = self._packed
+        if hasattr(p, "device") and not isinstance(p, np.ndarray):
+            p = p.cpu().numpy()
+        p = np.ascontiguousarray(p).view(np.uint64).reshape(-1, max(W, 1))
+        return np.unique(p, axis=0) if len(p) else p
+
+    # pickling (run_legacy_or_retrieve dumps the returned tuple, analysis.py:284-290): only host
+    # data -- the distinct panels as packed rows (or the materialised set) -- so the pickle loads
+    # on a machine without a GPU
+    def __getstate__(self):
+        st = {"count": self._count, "n": self._n, "ids": self._ids}
+        if self._set is not None:
+            st["set"] = self._set
+        else:
+            st["rows"] = self.rows()
+        return st
+
+    def __setstate__(self, st):
+        self._count, self._n, self._ids = st["count"], st["n"], st["ids"]
+        self._set = st.get("set")
+        self._packed = st.get("rows")
 
 
 def _with_address(enc, columns_data, check_same_address_columns):
@@ -218,10 +256,27 @@ def legacy_find_batch(feature_info, agents, k, count, max_attempts=0, rng: str =
 
 
 class LegacyRaw:
-    """Integer results of one legacy_probabilities run (exact, before division)."""
+    """Integer results of one legacy_probabilities run (exact, before division).  ``stats``: the
+    run's draw statistics (attempts, SelectionErrors, min-quota rejections; see draw_stats)."""
 
-    def __init__(self, counts, pairs, unique, panels, attempts):
+    def __init__(self, counts, pairs, unique, panels, attempts, stats=None):
         self.counts, self.pairs, self.unique, self.panels, self.attempts = counts, pairs, unique, panels, attempts
+        self.stats = stats
+
+
+STAT_KEYS = ("attempts", "selection_errors", "rejections")
+# draw statistics of the last legacy_probabilities call (SURVEY.md section 5 "Metrics"): the
+# reference prints "Rejected" per min-quota rejection (analysis.py:159) and restarts silently on a
+# SelectionError (analysis.py:152-153); here both are counted on the device
+LAST_RUN_STATS = None
+
+
+def draw_stats(enc, reset=False):
+    """Totals of the instance's draws since creation / the last reset (csa_instance_draw_stats):
+    {"attempts", "selection_errors", "rejections"}.  Synchronises the device."""
+    out = np.zeros(3, np.uint64)
+    N.check(N.lib().csa_instance_draw_stats(enc.handle, 1 if reset else 0, N.ptr(out)))
+    return dict(zip(STAT_KEYS, (int(x) for x in out)))
 
 
 def legacy_sample_raw(enc, k, iterations, random_seed, panel_begin=0, want_pairs=True, want_panels=True,
@@ -242,6 +297,7 @@ def legacy_sample_raw(enc, k, iterations, random_seed, panel_begin=0, want_pairs
         flags |= N.CSA_WANT_PANELS
     seed64 = int(random_seed) & 0xFFFFFFFFFFFFFFFF
     outs = (N.ptr(panels), N.ptr(counts), N.ptr(pairs), N.ptr(unique), N.ptr(attempts))
+    draw_stats(enc, reset=True)
     if devices is None:
         rc = N.lib().csa_legacy_sample(enc.handle, int(k), seed64, panel_begin, S, flags, max_attempts, *outs)
     else:
@@ -253,17 +309,19 @@ def legacy_sample_raw(enc, k, iterations, random_seed, panel_begin=0, want_pairs
     if rc == N.CSA_E_NO_CANDIDATE:
         raise KeyError("")                       # legacy.py:188
     N.check(rc)
-    return LegacyRaw(counts, pairs, int(unique[0]), panels, attempts)
+    return LegacyRaw(counts, pairs, int(unique[0]), panels, attempts, draw_stats(enc))
 
 
-def legacy_sample_device(enc, k, S, random_seed, keep_panels=True, chunk=1 << 20, host_panels=None):
+def legacy_sample_device(enc, k, S, random_seed, keep_panels=True, chunk=1 << 20, host_panels=None,
+                         host_stats=None):
     """One legacy_probabilities batch on the device through a DevicePipeline cached with the
     encoding (picks / XT / scratch buffers reused across calls).  Panels and hashes of the whole
     batch go to fresh device tensors (the exact distinct count needs all of them; with
     ``keep_panels`` the returned PanelSet keeps the panel tensor and decodes it only when
     iterated).  Returns LegacyRaw with host counts and device pair counts (PairHistogram
     materialises them lazily).  ``host_panels`` (uint64[S, W], MT mode: drawn on the host)
-    replaces the device draw; the counting, pairs and distinct count still run on the device."""
+    replaces the device draw; the counting, pairs and distinct count still run on the device
+    (``host_stats``: that draw's statistics)."""
     import torch
     from .device import DevicePipeline
     from .distributed import HashTable
@@ -271,7 +329,8 @@ def legacy_sample_device(enc, k, S, random_seed, keep_panels=True, chunk=1 << 20
     pipe = getattr(enc, "_pipe", None)
     C = max(1, min(S, int(chunk)))
     if pipe is None or pipe.max_panels < C or pipe.k != int(k):
-        pipe = enc._pipe = DevicePipeline(enc, k, C, want_pairs=True, want_unique=True)
+        # want_pairs for the XT / pair scratch; the n*n pair matrix is a fresh tensor per call
+        pipe = enc._pipe = DevicePipeline(enc, k, C, want_pairs=True, want_unique=True, pairs_buffer=False)
     W = enc.W
     dev = pipe.device
     with torch.cuda.device(dev), torch.cuda.stream(pipe.stream):
@@ -279,6 +338,8 @@ def legacy_sample_device(enc, k, S, random_seed, keep_panels=True, chunk=1 << 20
         hashes = torch.empty(max(2 * S, 2), dtype=torch.int64, device=dev)
         pairs = torch.empty(enc.n * enc.n, dtype=torch.int64, device=dev)
         pipe.reset(pairs=False)
+        if host_panels is None:
+            draw_stats(enc, reset=True)
         own_p, own_h, own_pairs = pipe.panels, pipe.hashes, pipe.pairs
         pipe.pairs = pairs
         try:
@@ -306,9 +367,11 @@ def legacy_sample_device(enc, k, S, random_seed, keep_panels=True, chunk=1 << 20
             counts = pipe.counts.cpu().numpy()       # synchronises the stream
             unique = int(table.count.item())
             pipe.check_status()
+            stats = draw_stats(enc) if host_panels is None else host_stats
         finally:
             pipe.panels, pipe.hashes, pipe.pairs = own_p, own_h, own_pairs
-    return LegacyRaw(counts, pairs.view(enc.n, enc.n), unique, panels[: S * W] if keep_panels else None, None)
+    return LegacyRaw(counts, pairs.view(enc.n, enc.n), unique, panels[: S * W] if keep_panels else None, None,
+                     stats)
 
 
 def legacy_probabilities(instance: Instance, iterations: int, random_seed: int,
@@ -341,8 +404,10 @@ def legacy_probabilities(instance: Instance, iterations: int, random_seed: int,
         random.seed(random_seed)
         np.random.seed(random_seed)                  # analysis.py:170 (unused by LEGACY)
         enc.check_quotas(instance.k)
-        picks, panels, _ = mt_draw(enc, instance.k, S)
-        raw = legacy_sample_device(enc, instance.k, S, random_seed, keep_panels=keep_panels, host_panels=panels)
+        st = np.zeros(3, np.uint64)
+        picks, panels, _ = mt_draw(enc, instance.k, S, stats=st)
+        raw = legacy_sample_device(enc, instance.k, S, random_seed, keep_panels=keep_panels, host_panels=panels,
+                                   host_stats=dict(zip(STAT_KEYS, (int(x) for x in st))))
         return finish(instance, enc, raw, S)
     if D.world_size() > 1:
         return D.legacy_probabilities_distributed(instance, iterations, random_seed, keep_panels=keep_panels)
@@ -358,6 +423,8 @@ def legacy_probabilities(instance: Instance, iterations: int, random_seed: int,
 
 
 def finish(instance, enc, raw, S):
+    global LAST_RUN_STATS
+    LAST_RUN_STATS = raw.stats
     alloc = {aid: int(raw.counts[p]) / S for p, aid in enumerate(enc.agent_ids)}
     hist = PairHistogram(len(instance.agents), counts=raw.pairs)
     hist.turn_into_probabilities_by_dividing_all_elements_by_given_number(S)

@@ -131,6 +131,9 @@ struct DrawArgs {
     int32_t *picks;            // n_panels x k or null
     uint16_t *picks16;         // draw_lane_kernel: n_panels x k pick lists (picks_pack_kernel -> panels)
     uint32_t *status;          // 4 words
+    // draw statistics (csa_instance_draw_stats): [0] SelectionError restarts, [1] min-quota
+    // rejections; one fire-and-forget atomic per restart (null: not counted)
+    unsigned long long *stats;
     int32_t *sel_out, *rem_out;
     uint64_t *present_out;
 };
@@ -522,6 +525,7 @@ __global__ __launch_bounds__(draw_threads(FPL, WPL), draw_occupancy(FPL, WPL)) v
                     active = false;
                 } else if (outcome != kAccept) {  // SelectionError restart / min-quota rejection
                     s = 0;
+                    if (glane == 0 && A.stats) atomicAdd(A.stats + (outcome == kReject), 1ull);
                     if (++a >= max_att) {
                         if (glane == 0) raise_status(A.status, CSA_E_ATTEMPT_LIMIT, panel);
                         active = false;
@@ -888,10 +892,13 @@ __device__ __forceinline__ bool uq_valid(uint64_t i, uint32_t seg_cap, const uin
 
 // one thread per panel: open addressing on `panel index + 1`, keyed by the 128-bit hash, exact
 // bitmask comparison on a hash match (small batches; the XMIN portfolio table)
+// With rep (the exchange's local distinct set beyond the partitioned path's size): the index of every
+// inserted (first-seen) panel goes to rep[], one rep_count atomic per wave.
 __global__ void unique_kernel(const uint64_t *__restrict__ hashes, const uint64_t *__restrict__ panels,
                               uint64_t S, int W, unsigned long long *__restrict__ table,
                               uint64_t mask, unsigned long long *__restrict__ unique, uint32_t seg_cap,
-                              const uint64_t *__restrict__ seg_counts) {
+                              const uint64_t *__restrict__ seg_counts, uint32_t *__restrict__ rep,
+                              unsigned long long *__restrict__ rep_count) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     bool inserted = false;
     if (i < S && uq_valid(i, seg_cap, seg_counts)) {
@@ -913,7 +920,13 @@ __global__ void unique_kernel(const uint64_t *__restrict__ hashes, const uint64_
         }
     }
     const uint64_t b = __ballot(inserted);
-    if ((threadIdx.x & 63) == 0 && b) atomicAdd(unique, (unsigned long long)__popcll(b));
+    if (unique && (threadIdx.x & 63) == 0 && b) atomicAdd(unique, (unsigned long long)__popcll(b));
+    if (rep) {
+        unsigned long long base = 0;
+        if ((threadIdx.x & 63) == 0 && b) base = atomicAdd(rep_count, (unsigned long long)__popcll(b));
+        base = __shfl(base, 0);
+        if (inserted) rep[base + __popcll(b & ((1ull << (threadIdx.x & 63)) - 1ull))] = (uint32_t)i;
+    }
 }
 
 // ---- partitioned distinct count (no global atomics per panel) -----------------------------
@@ -1266,6 +1279,10 @@ struct csa_instance {
     uint64_t gen = 1;
     std::vector<csa_instance *> replicas;  // [shard] (null: the instance itself / not created)
     std::vector<uint64_t> replica_gen;
+    // draw statistics (csa_instance_draw_stats): device counters of SelectionError restarts and
+    // min-quota rejections (DrawArgs::stats), host tally of the panels the batch draws accepted
+    unsigned long long *d_stats = nullptr;
+    uint64_t panels_drawn = 0;
 };
 
 namespace {
@@ -1543,6 +1560,7 @@ int launch_draw(const csa_instance *I, int32_t k, uint64_t seed, uint64_t panel_
             HIPCHK(hipGetLastError());
             return CSA_OK;
         }
+        if (!rejected) const_cast<csa_instance *>(I)->panels_drawn += n_panels;
         HIPCHK(hipMemsetAsync(d_panels, 0, n_panels * I->W * 8, stream));
         hipLaunchKernelGGL(empty_panels_kernel, dim3((unsigned)((n_panels + 255) / 256)), dim3(256), 0, stream,
                            n_panels, d_attempts, d_status, panel_begin, rejected);
@@ -1583,6 +1601,8 @@ int launch_draw(const csa_instance *I, int32_t k, uint64_t seed, uint64_t panel_
     A.picks = d_picks;
     A.picks16 = nullptr;
     A.status = d_status;
+    // legacy_find-semantics draws are counted; single attempts (csa_legacy_attempt) are not
+    A.stats = single ? nullptr : I->d_stats;
     A.sel_out = d_sel_out;
     A.rem_out = d_rem_out;
     A.present_out = d_present_out;
@@ -1623,6 +1643,7 @@ int launch_draw(const csa_instance *I, int32_t k, uint64_t seed, uint64_t panel_
     void *args[] = {&A};
     HIPCHK(hipLaunchKernel(cfg.fn, dim3((unsigned)std::max<uint64_t>(1, grid)), dim3(threads), args, lds, stream));
     HIPCHK(hipGetLastError());
+    if (!single) M->panels_drawn += n_panels;
     if (cfg.picks() && !d_picks_ext) {  // pick lists -> packed panels (+ hashes)
         if (!fused && (rc = launch_pack(A.picks16, n_panels, k, I->W, d_panels, d_hashes, stream))) return rc;
         HIPCHK(hipEventRecord(M->picks_done, stream));
@@ -1733,7 +1754,7 @@ int unique_impl(const uint64_t *d_hashes, const uint64_t *d_panels, uint64_t n_p
     const unsigned grid = (unsigned)((n_panels + 255) / 256);
     hipLaunchKernelGGL(unique_kernel, dim3(grid), dim3(256), 0, st, d_hashes, d_panels, n_panels, W,
                        reinterpret_cast<unsigned long long *>(d_table), table_slots - 1,
-                       reinterpret_cast<unsigned long long *>(d_unique), seg_cap, seg_counts);
+                       reinterpret_cast<unsigned long long *>(d_unique), seg_cap, seg_counts, nullptr, nullptr);
     HIPCHK(hipGetLastError());
     return CSA_OK;
 }
@@ -1810,7 +1831,8 @@ int csa_instance_create(int32_t n, int32_t C, int32_t F, const int32_t *person_f
     int rc = CSA_OK;
     if ((rc = dalloc(&I->d_featmask, I->featmask.size())) || (rc = dalloc(&I->d_fmin, F)) ||
         (rc = dalloc(&I->d_fmax, F)) || (rc = dalloc(&I->d_sel0, F)) || (rc = dalloc(&I->d_rem0, F)) ||
-        (rc = dalloc(&I->d_present0, I->W)) || (F <= 32 && (rc = dalloc(&I->d_pmask, n)))) {
+        (rc = dalloc(&I->d_present0, I->W)) || (F <= 32 && (rc = dalloc(&I->d_pmask, n))) ||
+        (rc = dalloc(&I->d_stats, 2))) {
         csa_instance_destroy(I);
         return rc;
     }
@@ -1825,6 +1847,7 @@ int csa_instance_create(int32_t n, int32_t C, int32_t F, const int32_t *person_f
     e = e ? e : hipMemcpy(I->d_rem0, I->pool.data(), F * 4, hipMemcpyHostToDevice);
     if (I->W) e = e ? e : hipMemcpy(I->d_present0, present.data(), I->W * 8, hipMemcpyHostToDevice);
     if (!pmask.empty()) e = e ? e : hipMemcpy(I->d_pmask, pmask.data(), pmask.size() * 4, hipMemcpyHostToDevice);
+    e = e ? e : hipMemset(I->d_stats, 0, 16);
     if (e != hipSuccess) {
         csa_instance_destroy(I);
         return fail(CSA_E_HIP, "instance upload: %s", hipGetErrorString(e));
@@ -1850,6 +1873,7 @@ void csa_instance_destroy(csa_instance *I) {
     if (I->d_pmask) (void)hipFree(I->d_pmask);
     if (I->d_addr_next) (void)hipFree(I->d_addr_next);
     if (I->d_picks16) (void)hipFree(I->d_picks16);
+    if (I->d_stats) (void)hipFree(I->d_stats);
     for (int i = 0; i < kScratchSlots; ++i)
         if (I->scratch[i]) (void)hipFree(I->scratch[i]);
     if (I->picks_done) (void)hipEventDestroy(I->picks_done);
@@ -1860,6 +1884,29 @@ void csa_instance_destroy(csa_instance *I) {
     for (csa_instance *R : I->replicas)
         if (R) csa_instance_destroy(R);
     delete I;
+}
+
+int csa_instance_draw_stats(csa_instance *I, int32_t reset, uint64_t *out) {
+    if (!I || !out) return fail(CSA_E_INVALID, "draw_stats: bad arguments");
+    uint64_t acc[3] = {0, 0, 0};
+    std::vector<csa_instance *> all{I};
+    for (csa_instance *R : I->replicas)
+        if (R) all.push_back(R);
+    for (csa_instance *X : all) {
+        ScopedDevice sd(X->device);
+        HIPCHK(hipDeviceSynchronize());  // every stream that may still run a draw of X
+        unsigned long long h[2];
+        HIPCHK(hipMemcpy(h, X->d_stats, 16, hipMemcpyDeviceToHost));
+        acc[0] += X->panels_drawn + h[0] + h[1];
+        acc[1] += h[0];
+        acc[2] += h[1];
+        if (reset) {
+            HIPCHK(hipMemset(X->d_stats, 0, 16));
+            X->panels_drawn = 0;
+        }
+    }
+    for (int j = 0; j < 3; ++j) out[j] = acc[j];
+    return CSA_OK;
 }
 
 int csa_instance_info(const csa_instance *I, int32_t *n, int32_t *C, int32_t *F, int32_t *W) {
@@ -2172,10 +2219,18 @@ int csa_unique_segments_async(const uint64_t *d_hashes, const uint64_t *d_panels
                        d_status, (uint32_t)capacity, d_seg_counts, (hipStream_t)stream);
 }
 
-uint64_t csa_exchange_scratch_bytes(uint64_t n_panels) {
+// scratch of csa_exchange_pack_async: rep_count, rep[n], then the partitioned pass's scratch or --
+// for a shard beyond it (more than 2048 panels per partition at the 8192-partition maximum, i.e.
+// above 16.8 M panels) -- one global open-addressing table of pow2 >= 2n slots
+static uint64_t exchange_dedupe_bytes(uint64_t n) {
     UqPlan q;
-    uq_plan(std::max<uint64_t>(n_panels, 1), q);
-    return 8 + 4 * std::max<uint64_t>(n_panels, 1) + q.scratch_bytes + 8;
+    uq_plan(n, q);
+    return q.fits ? q.scratch_bytes : 8 * pow2_at_least(std::max<uint64_t>(2 * n, 64));
+}
+
+uint64_t csa_exchange_scratch_bytes(uint64_t n_panels) {
+    const uint64_t n = std::max<uint64_t>(n_panels, 1);
+    return 8 + 4 * (n + 1) + exchange_dedupe_bytes(n) + 8;
 }
 
 int csa_exchange_pack_async(const uint64_t *d_hashes, const uint64_t *d_panels, uint64_t n_panels, int32_t W,
@@ -2185,7 +2240,7 @@ int csa_exchange_pack_async(const uint64_t *d_hashes, const uint64_t *d_panels, 
     if (!d_hashes || !d_panels || W <= 0 || world == 0 || world > (uint32_t)kMaxWorld || capacity == 0 ||
         !d_scratch || !d_send_hashes || !d_send_panels || !d_send_counts || !d_status)
         return fail(CSA_E_INVALID, "exchange pack: bad arguments");
-    if (n_panels >= (1ull << 31)) return fail(CSA_E_UNSUPPORTED, "exchange pack: n_panels >= 2^31");
+    if (n_panels >= (1ull << 31)) return fail(CSA_E_UNSUPPORTED, "exchange pack: n_panels >= 2^31 (u32 indices)");
     if (scratch_bytes < csa_exchange_scratch_bytes(n_panels))
         return fail(CSA_E_INVALID, "exchange pack: scratch_bytes < csa_exchange_scratch_bytes(n_panels)");
     const hipStream_t st = (hipStream_t)stream;
@@ -2198,8 +2253,18 @@ int csa_exchange_pack_async(const uint64_t *d_hashes, const uint64_t *d_panels, 
     // 1. the local distinct panels (exact: hash AND bitmask), their indices into rep[]
     UqPlan q;
     uq_plan(n_panels, q);
-    int rc = uq_partitioned(d_hashes, d_panels, n_panels, W, q, part, nullptr, d_status, 0, nullptr, rep, rep_count, st);
-    if (rc) return rc;
+    if (q.fits) {
+        int rc = uq_partitioned(d_hashes, d_panels, n_panels, W, q, part, nullptr, d_status, 0, nullptr, rep, rep_count,
+                                st);
+        if (rc) return rc;
+    } else {  // beyond the partitioned path: one global table, first-seen indices listed in rep[]
+        const uint64_t slots = pow2_at_least(std::max<uint64_t>(2 * n_panels, 64));
+        unsigned long long *table = reinterpret_cast<unsigned long long *>(part);
+        HIPCHK(hipMemsetAsync(table, 0, slots * 8, st));
+        hipLaunchKernelGGL(unique_kernel, dim3((unsigned)((n_panels + 255) / 256)), dim3(256), 0, st, d_hashes, d_panels,
+                           n_panels, W, table, slots - 1, nullptr, 0u, nullptr, rep, rep_count);
+        HIPCHK(hipGetLastError());
+    }
     // 2. bucket them by owner into the fixed-capacity segments
     const unsigned grid = (unsigned)((n_panels + kXbThreads - 1) / kXbThreads);
     hipLaunchKernelGGL(exchange_bucket_kernel, dim3(grid), dim3(kXbThreads), 0, st, d_hashes, d_panels, W, rep,

@@ -189,7 +189,9 @@ int csa_legacy_draw_mt(int32_t n, int32_t C, int32_t F, const int32_t *person_fe
                        const int32_t *fmax, const int32_t *sel0, const int32_t *rem0, const uint64_t *present0,
                        const int32_t *addr_next, int32_t k, uint32_t *mt_state, uint64_t n_panels,
                        uint32_t max_attempts, int32_t single, int32_t *picks_out, uint64_t *panels_out,
-                       uint32_t *attempts_out, int32_t *sel_out, int32_t *rem_out, uint64_t *present_out) {
+                       uint32_t *attempts_out, int32_t *sel_out, int32_t *rem_out, uint64_t *present_out,
+                       uint64_t *stats_out) {
+    if (stats_out) stats_out[0] = stats_out[1] = stats_out[2] = 0;
     if (n < 0 || C <= 0 || F <= 0 || k < 0 || !person_feat || !fmin || !fmax || !mt_state ||
         mt_state[kMtN] > (uint32_t)kMtN) {
         return fail(CSA_E_INVALID, "draw_mt: bad arguments");
@@ -235,12 +237,14 @@ int csa_legacy_draw_mt(int32_t n, int32_t C, int32_t F, const int32_t *person_fe
             pool.assign(q0, q0 + I.W);
             const int st = attempt(I, k, rng, sel, rem, pool, picks);
             ++a;
+            if (stats_out) ++stats_out[0];
             if (st == kNoCand) {
                 return fail(CSA_E_NO_CANDIDATE, "panel " + std::to_string(i) +
                                                     ": no candidate feature while agents remain (KeyError, legacy.py:188)");
             }
             if (single) {
                 if (st == kFail) {
+                    if (stats_out) ++stats_out[1];
                     return fail(CSA_E_SELECTION, "SelectionError (legacy.py:34)");
                 }
                 break;
@@ -248,6 +252,7 @@ int csa_legacy_draw_mt(int32_t n, int32_t C, int32_t F, const int32_t *person_fe
             bool under = false;  // check_min_cats (legacy.py:160-168)
             for (int f = 0; f < F; ++f) under |= sel[f] < fmin[f];
             if (st == kOk && !under) break;
+            if (stats_out) ++stats_out[st == kOk ? 2 : 1];  // rejection ("Rejected") / SelectionError
             if (a >= cap) {
                 return fail(CSA_E_ATTEMPT_LIMIT,
                             "panel " + std::to_string(i) + ": attempt limit reached without an accepted panel");

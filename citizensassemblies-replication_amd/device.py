@@ -30,7 +30,9 @@ def _stream_ptr(stream):
 
 class DevicePipeline:
     def __init__(self, enc, k, max_panels, want_pairs=True, want_unique=True, want_attempts=False,
-                 device=None, stream=None, pair_engine=N.CSA_PAIR_FP4):
+                 device=None, stream=None, pair_engine=N.CSA_PAIR_FP4, pairs_buffer=True):
+        """``pairs_buffer=False``: no n*n pair matrix of its own (the caller sets ``self.pairs``
+        before ``pair_counts``); XT and the pair scratch are still allocated with want_pairs."""
         self.enc = enc
         self.k = int(k)
         self.device = torch.device(device or "cuda")
@@ -62,7 +64,7 @@ class DevicePipeline:
             self.status = torch.zeros(4, dtype=torch.int32, device=dev)
             self.counts = torch.zeros(n, dtype=torch.int64, device=dev)
             self.xt = torch.empty(nblk * self.npad, dtype=u64, device=dev) if want_pairs else None
-            self.pairs = torch.zeros(n * n, dtype=torch.int64, device=dev) if want_pairs else None
+            self.pairs = torch.zeros(n * n, dtype=torch.int64, device=dev) if want_pairs and pairs_buffer else None
             sb = int(L.csa_pair_scratch_bytes(max(n, 1), max(nblk, 1), self.pair_engine)) if want_pairs else 0
             self.pair_scratch = torch.empty((sb + 3) // 4, dtype=torch.int32, device=dev) if want_pairs else None
             self.table = torch.empty(slots, dtype=u64, device=dev) if want_unique else None

@@ -308,28 +308,97 @@ def combine(counts, pairs, hashes, panels, W, exchange=None, stream=None, pair_b
     return counts, pairs, u
 
 
-def gather_panels(panels, S, W):
-    """All ranks' shards (contiguous global ranges, shard_range) -> uint64[S, W] on every rank."""
+def _raise_together(status, stream=None):
+    """Every rank raises when any rank's status block holds an error: all_reduce(MAX) of the error
+    code first, so no rank goes on into a collective that the failing rank never joins.  The failing
+    rank raises its own decoded error; the others the same code (KeyError for a missing candidate,
+    legacy.py:188)."""
     import torch
     import torch.distributed as dist
-    world = dist.get_world_size()
-    per = shard_range(S, world, 0)[1]
-    buf = torch.zeros(per * W, dtype=torch.int64, device=panels.device)
-    buf[: panels.numel()] = panels
-    src = buf.cpu() if _host_collectives(buf) else buf
-    parts = [torch.empty_like(src) for _ in range(world)]
-    dist.all_gather(parts, src)
-    rows = []
-    for r, t in enumerate(parts):
-        b, e = shard_range(S, world, r)
-        rows.append(t.cpu().numpy().view(np.uint64).reshape(per, W)[: e - b])
-    return np.concatenate(rows) if rows else np.zeros((0, W), np.uint64)
+    from . import _native as N
+    if stream is not None:
+        stream.synchronize()
+    code = status[:1].to(torch.int64)
+    _all_reduce(code, op=dist.ReduceOp.MAX)
+    c = int(code.item())
+    if not c:
+        return
+    h = status.cpu().numpy().astype(np.uint32)
+    if int(h[0]) == 0:                       # another rank failed: report its code
+        h = np.array([c, 0xFFFFFFFF, 0xFFFFFFFF, 0], np.uint32)
+    rc = N.lib().csa_status_decode(N.ptr(h))
+    if rc == N.CSA_E_NO_CANDIDATE:
+        raise KeyError("")
+    N.check(rc)
+
+
+def local_distinct_rows(hashes, panels, n, W, status=None, stream=None):
+    """This rank's exact distinct panels (hash AND bitmask): (uint64 rows as an int64 tensor of
+    count*W words on the inputs' device, count).  Device inputs: csa_exchange_pack_async with one
+    owner (the partitioned dedupe + bucketing of the exchange); host inputs: local_distinct."""
+    import torch
+    n, W = int(n), int(W)
+    if not hashes.is_cuda:
+        _, p = local_distinct(hashes.numpy().view(np.uint64)[: 2 * n], panels.numpy().view(np.uint64)[: n * W]
+                              .reshape(n, W))
+        return torch.from_numpy(np.ascontiguousarray(p).view(np.int64).reshape(-1)), len(p)
+    from . import _native as N
+    dev = hashes.device
+    st = stream or torch.cuda.current_stream(dev)
+    m = max(n, 1)
+    send_h = torch.empty(2 * m, dtype=torch.int64, device=dev)
+    send_p = torch.empty(m * W, dtype=torch.int64, device=dev)
+    send_c = torch.zeros(1, dtype=torch.int64, device=dev)
+    sb = int(N.lib().csa_exchange_scratch_bytes(m))
+    scratch = torch.empty((sb + 7) // 8, dtype=torch.int64, device=dev)
+    own_status = status if status is not None else torch.zeros(4, dtype=torch.int32, device=dev)
+    N.check(N.lib().csa_exchange_pack_async(N.ptr(hashes), N.ptr(panels), n, W, 1, m, N.ptr(scratch), sb,
+                                            N.ptr(send_h), N.ptr(send_p), N.ptr(send_c), N.ptr(own_status),
+                                            ctypes.c_void_p(st.cuda_stream)))
+    st.synchronize()
+    if status is None:
+        h = own_status.cpu().numpy().astype(np.uint32)
+        N.check(N.lib().csa_status_decode(N.ptr(h)))
+    cnt = int(send_c.item())
+    return send_p[: cnt * W], cnt
+
+
+def gather_distinct_to_root(hashes, panels, n, W, status=None, stream=None):
+    """found_panels of a sharded run, on rank 0 only: every rank reduces its shard to its exact local
+    distinct panels, and rank 0 receives them one rank at a time (a buffer sized for that rank, copied
+    to the host before the next), so no rank ever holds the whole job's panels on its device.
+    Returns uint64[m, W] on rank 0 (rows of all ranks; a panel drawn on two ranks appears twice and
+    PanelSet deduplicates on iteration), None elsewhere."""
+    import torch
+    import torch.distributed as dist
+    world, r = dist.get_world_size(), dist.get_rank()
+    rows, cnt = local_distinct_rows(hashes, panels, n, W, status, stream)
+    host = _host_collectives(rows) or not rows.is_cuda
+    dev = torch.device("cpu") if host else rows.device
+    if r != 0:
+        dist.send(torch.tensor([cnt], dtype=torch.int64, device=dev), 0)
+        if cnt:
+            dist.send(rows.cpu() if host else rows.contiguous(), 0)
+        return None
+    parts = [rows.cpu().numpy().view(np.uint64).reshape(cnt, W)]
+    for src in range(1, world):
+        c = torch.zeros(1, dtype=torch.int64, device=dev)
+        dist.recv(c, src)
+        c = int(c.item())
+        if c:
+            buf = torch.empty(c * W, dtype=torch.int64, device=dev)
+            dist.recv(buf, src)
+            parts.append(buf.cpu().numpy().view(np.uint64).reshape(c, W))
+            del buf
+    return np.concatenate(parts)
 
 
 def legacy_probabilities_distributed(instance, iterations, random_seed, keep_panels=True):
     """analysis.py:162-191 with the panels sharded over the ranks of the default group.  Every rank
-    returns the whole job's results; with ``keep_panels`` every rank gathers all panels so that
-    ``found_panels`` iterates like the reference's set (costs S*W*8 bytes per rank)."""
+    returns the whole job's alloc, pair histogram and exact distinct-panel count.  With
+    ``keep_panels`` rank 0's ``found_panels`` also iterates like the reference's set (the ranks'
+    exact local distinct panels are sent to rank 0, one rank at a time); on the other ranks it
+    supports len() only.  The draw statistics (analysis.LAST_RUN_STATS) are summed over ranks."""
     import torch
     from . import analysis as A
     from .device import DevicePipeline
@@ -346,14 +415,22 @@ def legacy_probabilities_distributed(instance, iterations, random_seed, keep_pan
     torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", r)) % max(torch.cuda.device_count(), 1))
     pipe = DevicePipeline(enc, instance.k, max(local, 1), want_pairs=True, want_unique=True)
     pipe.reset()
+    A.draw_stats(enc, reset=True)
     if local:
         pipe.draw(random_seed, begin, local)
         pipe.transpose_count(local)
         pipe.pair_counts(local)
-    pipe.check_status()
+    _raise_together(pipe.status, pipe.stream)
     counts, pairs, u = combine(pipe.counts, pipe.pairs, pipe.hashes[: 2 * local], pipe.panels[: local * enc.W],
                                enc.W, pair_bound=S, status=pipe.status)
-    pipe.check_status()
-    panels = gather_panels(pipe.panels[: local * enc.W], S, enc.W) if keep_panels else None
-    raw = A.LegacyRaw(counts.cpu().numpy(), pairs.cpu().numpy().reshape(enc.n, enc.n), int(u.item()), panels, None)
-    return A.finish(instance, enc, raw, S)
+    _raise_together(pipe.status, pipe.stream)
+    stats = torch.tensor(list(A.draw_stats(enc).values()), dtype=torch.int64, device=pipe.counts.device)
+    _all_reduce(stats)
+    panels = gather_distinct_to_root(pipe.hashes[: 2 * local], pipe.panels[: local * enc.W], local, enc.W,
+                                     pipe.status, pipe.stream) if keep_panels else None
+    raw = A.LegacyRaw(counts.cpu().numpy(), pairs.cpu().numpy().reshape(enc.n, enc.n), int(u.item()), panels, None,
+                      dict(zip(A.STAT_KEYS, (int(x) for x in stats.cpu().tolist()))))
+    out = A.finish(instance, enc, raw, S)
+    if keep_panels and r != 0:
+        out[1]._where = "found_panels of a sharded run iterate on rank 0 only (len() is global)"
+    return out

@@ -102,6 +102,11 @@ class EncodedInstance:
                 N.check(L.csa_instance_set_state(h, N.ptr(self.sel0), N.ptr(self.rem0), None))
         return self._handle
 
+    def release_device_buffers(self):
+        """Drop the cached device pipeline / hash table (they are rebuilt on the next call)."""
+        self.__dict__.pop("_pipe", None)
+        self.__dict__.pop("_table", None)
+
     def close(self):
         if self._handle is not None:
             N.lib().csa_instance_destroy(self._handle)
@@ -156,6 +161,10 @@ def encode_cached(categories, agents) -> EncodedInstance:
             return enc
     enc = EncodedInstance(categories, agents)
     _ENC_CACHE.append((categories, agents, fp, enc))
+    for entry in _ENC_CACHE[:-_ENC_CACHE_SIZE]:
+        # an evicted entry's device buffers (analysis.legacy_sample_device's pipeline and
+        # distinct-count table) go now, not when the last reference to the encoding goes
+        entry[3].release_device_buffers()
     del _ENC_CACHE[:-_ENC_CACHE_SIZE]
     return enc
 

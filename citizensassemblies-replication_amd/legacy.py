@@ -75,12 +75,13 @@ def seed(seed_value):
     STREAM.seed(seed_value)
 
 
-def mt_draw(enc, k, n_panels, single=False, max_attempts=0, state=False, addr_next=None):
+def mt_draw(enc, k, n_panels, single=False, max_attempts=0, state=False, addr_next=None, stats=None):
     """MT19937 mode: ``n_panels`` legacy_find calls (``single``: one find_random_sample_legacy
     call) drawing from the stdlib ``random`` module's global state exactly as legacy.py:149
     does; the state is advanced in place (random.setstate), also when the draw raises.
     Returns (picks int32[n_panels, k], panels uint64[n_panels, W], attempts) and, with
-    ``state``, the final (sel, rem, present) of the single attempt."""
+    ``state``, the final (sel, rem, present) of the single attempt.  ``stats`` (uint64[3], optional)
+    receives the call's attempts, SelectionErrors and min-quota rejections."""
     import random
     k = int(k)
     st = random.getstate()
@@ -96,7 +97,7 @@ def mt_draw(enc, k, n_panels, single=False, max_attempts=0, state=False, addr_ne
                                         N.ptr(enc.sel0), N.ptr(enc.rem0), None, N.ptr(addr_next), k, N.ptr(words),
                                         int(n_panels),
                                         max_attempts, 1 if single else 0, N.ptr(picks), N.ptr(panels),
-                                        N.ptr(attempts), N.ptr(sel), N.ptr(rem), N.ptr(present))
+                                        N.ptr(attempts), N.ptr(sel), N.ptr(rem), N.ptr(present), N.ptr(stats))
     finally:
         random.setstate((st[0], tuple(int(x) for x in words), st[2]))
     if rc == N.CSA_E_SELECTION:

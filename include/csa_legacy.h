@@ -74,6 +74,18 @@ int csa_instance_info(const csa_instance *inst, int32_t *n, int32_t *C, int32_t 
 int csa_instance_set_state(csa_instance *inst, const int32_t *sel, const int32_t *rem,
                            const uint64_t *present);
 
+/* Draw statistics (SURVEY.md section 5 "Metrics"; the reference prints "Rejected" for every
+ * min-quota rejection, analysis.py:159, and restarts silently on SelectionError, analysis.py:152-153).
+ * Totals over every legacy_find-semantics draw launched on the instance -- csa_legacy_sample,
+ * csa_legacy_sample_devices (its per-device replicas included), csa_legacy_find,
+ * csa_first_panel_not_in, csa_draw_async / csa_draw_picks_async -- since creation or the last reset
+ * (csa_legacy_attempt's single attempts are not counted):
+ *   out[0] attempts = accepted panels + out[1] + out[2]
+ *   out[1] SelectionError restarts (legacy.py:34-36 raised inside an attempt)
+ *   out[2] min-quota rejections (check_min_cats false after k picks, legacy.py:160-168)
+ * Synchronises the instance's device(s); reset != 0 zeroes the totals after reading them. */
+int csa_instance_draw_stats(csa_instance *inst, int32_t reset, uint64_t *out);
+
 /* check_same_address (legacy.py:78-99, 103-113): addr_next (n int32) links the agents that share
  * an address (the check_same_address_columns values) into rings, agent order: addr_next[p] = the
  * next agent at p's address, p itself when p lives alone.  With a ring set, every pick deletes
@@ -152,12 +164,15 @@ int csa_first_panel_not_in(csa_instance *inst, int32_t k, uint64_t seed, uint64_
  * 0 / pool counts / everyone), addr_next the same-address rings (or NULL, see
  * csa_instance_set_address).  Outputs (each may be NULL): picks_out n_panels*k (pick order, -1
  * padded), panels_out n_panels*W, attempts_out n_panels; with single, the final sel/rem (F) and
- * remaining pool (W). */
+ * remaining pool (W); stats_out (3 uint64) the call's attempts, SelectionErrors and min-quota
+ * rejections, as csa_instance_draw_stats counts them (a single attempt that raises counts one
+ * SelectionError). */
 int csa_legacy_draw_mt(int32_t n, int32_t C, int32_t F, const int32_t *person_feat, const int32_t *fmin,
                        const int32_t *fmax, const int32_t *sel0, const int32_t *rem0, const uint64_t *present0,
                        const int32_t *addr_next, int32_t k, uint32_t *mt_state, uint64_t n_panels,
                        uint32_t max_attempts, int32_t single, int32_t *picks_out, uint64_t *panels_out,
-                       uint32_t *attempts_out, int32_t *sel_out, int32_t *rem_out, uint64_t *present_out);
+                       uint32_t *attempts_out, int32_t *sel_out, int32_t *rem_out, uint64_t *present_out,
+                       uint64_t *stats_out);
 
 /* ---- stream-ordered device API ---------------------------------------------
  * All buffers are device pointers on the instance's device; `stream` is a

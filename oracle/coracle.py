@@ -27,7 +27,7 @@ def lib():
         L.oracle_draw.restype = ctypes.c_int
         L.oracle_draw.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, P, P, P, P, ctypes.c_int,
                                   ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32,
-                                  P, P, P, ctypes.c_int]
+                                  P, P, P, P, ctypes.c_int]
         L.oracle_counts.restype = None
         L.oracle_counts.argtypes = [P, ctypes.c_uint64, ctypes.c_int, P]
         L.oracle_pairs.restype = None
@@ -58,8 +58,11 @@ def arrays(inst: OracleInstance):
             np.asarray(inst.fcat, np.int32))
 
 
-def draw(inst, k, seed, panel_begin, n_panels, max_attempts=1 << 20, want_picks=False, threads=None):
-    """Returns (status, panels uint64[S,W], attempts uint32[S], picks int32[S,k] or None)."""
+def draw(inst, k, seed, panel_begin, n_panels, max_attempts=1 << 20, want_picks=False, threads=None,
+         rejects=None):
+    """Returns (status, panels uint64[S,W], attempts uint32[S], picks int32[S,k] or None).
+    ``rejects`` (uint32[S], optional) receives each panel's min-quota rejections; the other
+    attempts - 1 restarts are SelectionErrors."""
     pf, fmin, fmax, fcat = arrays(inst)
     W = (inst.n + 63) // 64
     panels = np.zeros((n_panels, W), np.uint64)
@@ -68,7 +71,7 @@ def draw(inst, k, seed, panel_begin, n_panels, max_attempts=1 << 20, want_picks=
     threads = threads or os.cpu_count() or 1
     rc = lib().oracle_draw(inst.n, inst.C, inst.F, _ptr(pf), _ptr(fmin), _ptr(fmax), _ptr(fcat), k,
                            seed, panel_begin, n_panels, max_attempts, _ptr(panels), _ptr(picks),
-                           _ptr(attempts), threads)
+                           _ptr(attempts), _ptr(rejects), threads)
     return rc, panels, attempts, picks
 
 

@@ -150,7 +150,7 @@ static int attempt_once(const oinst *I, int k, uint64_t seed, uint64_t panel, ui
 int oracle_draw(int n, int C, int F, const int32_t *pf, const int32_t *fmin, const int32_t *fmax,
                 const int32_t *fcat, int k, uint64_t seed, uint64_t panel_begin, uint64_t n_panels,
                 uint32_t max_attempts, uint64_t *panels_out, int32_t *picks_out, uint32_t *attempts_out,
-                int nthreads) {
+                uint32_t *rejects_out, int nthreads) {
     if (n <= 0 || C <= 0 || F <= 0 || k < 0 || !pf || !fmin || !fmax || !fcat) return OR_E_INVALID;
     oinst I;
     I.n = n; I.C = C; I.F = F; I.W = (n + 63) / 64;
@@ -178,11 +178,12 @@ int oracle_draw(int n, int C, int F, const int32_t *pf, const int32_t *fmin, con
         for (int64_t i = 0; i < (int64_t)n_panels; ++i) {
             uint64_t panel = panel_begin + (uint64_t)i;
             int32_t *picks = picks_out ? picks_out + (size_t)i * k : NULL;
-            uint32_t a = 0;
+            uint32_t a = 0, rejects = 0;
             int rc = 1;
             for (; a < max_attempts; ++a) {
                 rc = attempt_once(&I, k, seed, panel, a, remaining, sel, rem, picked, del, picks);
                 if (rc == 0 || rc < 0) break;
+                rejects += rc == 2;  /* check_min_cats failed: "Rejected" (analysis.py:155-159) */
             }
             if (rc < 0) {
 #pragma omp atomic write
@@ -193,6 +194,7 @@ int oracle_draw(int n, int C, int F, const int32_t *pf, const int32_t *fmin, con
             }
             if (panels_out) memcpy(panels_out + (size_t)i * W, picked, sizeof(uint64_t) * W);
             if (attempts_out) attempts_out[i] = a + 1;
+            if (rejects_out) rejects_out[i] = rejects;
         }
         free(remaining); free(picked); free(del); free(sel); free(rem);
     }

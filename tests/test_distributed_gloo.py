@@ -57,7 +57,10 @@ def _worker(rank, world, port, out_dir, name):
     hashes = torch.from_numpy(D.panel_hashes(panels).ravel().view(np.int64).copy())
     ptens = torch.from_numpy(np.ascontiguousarray(panels).view(np.int64).ravel().copy())
     counts, pairs, u = D.combine(counts, pairs, hashes, ptens, W)
+    rows = D.gather_distinct_to_root(hashes, ptens, e - b, W)     # found_panels: rank 0 only
+    assert (rows is None) == (rank != 0)
     if rank == 0:
+        np.save(os.path.join(out_dir, "rows.npy"), rows)
         np.save(os.path.join(out_dir, "counts.npy"), counts.numpy())
         np.save(os.path.join(out_dir, "pairs.npy"), pairs.numpy())
         np.save(os.path.join(out_dir, "unique.npy"), np.array([int(u.item())]))
@@ -83,6 +86,10 @@ def test_gloo_exchange_matches_single_run(tmp_path, world, name):
         # duplicates really are split across ranks: every shard holds most of the 100 panels
         assert want == 100
     assert int(np.load(tmp_path / "unique.npy")[0]) == want
+    # the rows gathered on rank 0 (each rank's local distinct set) cover exactly the distinct panels
+    rows = np.load(tmp_path / "rows.npy")
+    assert len(rows) <= min(S, world * want)
+    assert np.array_equal(np.unique(rows, axis=0), np.unique(panels, axis=0))
 
 
 def _collision_worker(rank, world, port, out_dir):
@@ -160,3 +167,37 @@ def test_panel_hash_mirror_is_sensitive():
     q = p.copy()
     q[:, 5] ^= np.uint64(1)
     assert not np.any(np.all(D.panel_hashes(q) == h, axis=1))
+
+
+_RANK_SCRIPT = r"""
+import json, os, sys
+import torch, torch.distributed as dist
+dist.init_process_group("gloo")
+r, w = dist.get_rank(), dist.get_world_size()
+t = torch.tensor([r + 1])
+dist.all_reduce(t)
+if r == 0:
+    print(json.dumps({"world": w, "sum": int(t.item()), "argv": sys.argv[1:],
+                      "local": os.environ["LOCAL_RANK"], "addr": os.environ["MASTER_ADDR"]}))
+dist.destroy_process_group()
+"""
+
+
+def test_bench_self_launch_world2(tmp_path, capfd):
+    """bench.self_launch -- what `python bench.py --gpus 2` runs when no launcher set WORLD_SIZE --
+    starts two rank processes with RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 /
+    MASTER_PORT that rendezvous over gloo; the arguments reach every rank; exit code 0."""
+    import importlib.util
+    import json
+    spec = importlib.util.spec_from_file_location("bench", os.path.join(REPO, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    script = tmp_path / "rank.py"
+    script.write_text(_RANK_SCRIPT)
+    rc = bench.self_launch(2, script=str(script), argv=["--gpus", "2", "--steps", "1"])
+    assert rc == 0
+    line = [ln for ln in capfd.readouterr().out.splitlines() if ln.startswith("{")]
+    assert len(line) == 1
+    got = json.loads(line[0])
+    assert got == {"world": 2, "sum": 3, "argv": ["--gpus", "2", "--steps", "1"], "local": "0",
+                   "addr": "127.0.0.1"}

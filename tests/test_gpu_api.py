@@ -1,0 +1,198 @@
+"""GPU tests of the API surface around the hot path (round 3):
+
+  * the MT19937 product path -- legacy_probabilities(..., rng="mt"): host MT panels ->
+    csa_panel_hash_async -> device counts / pairs / exact distinct count -- against the
+    reference's PUBLISHED seed-0 probabilities and seed-1 unique counts (analysis.py:162-191
+    with random.seed at analysis.py:169, randint at legacy.py:149);
+  * csa_panel_hash_async called directly, against the host mirror distributed.panel_hashes;
+  * pickling of the returned tuple (run_legacy_or_retrieve, analysis.py:284-290): the pickle
+    holds host data only and loads in a process that sees no GPU;
+  * the draw statistics (attempts / SelectionErrors / min-quota rejections)
+    against the reference's own split (tests/golden/philox_*.json);
+  * the exchange's local distinct pass beyond the partitioned path (> 8192 x 2048 entries);
+  * bench.py --gpus 2 launching its own ranks (gloo rehearsal on one GPU) == the N = 1 run.
+"""
+import json
+import os
+import pickle
+import random
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from conftest import GOLD, REPO, golden, inst_paths, pkg
+
+pytestmark = pytest.mark.gpu
+
+with open(os.path.join(GOLD, "mt_published.json")) as fh:
+    MT = json.load(fh)
+
+
+def _inst(name, k):
+    return pkg().read_instance(*inst_paths(name), k)
+
+
+def _host_pairs(panels, n):
+    bits = np.unpackbits(np.ascontiguousarray(panels).view(np.uint8), axis=1, bitorder="little")[:, :n]
+    x = bits.astype(np.float64)
+    return np.rint(x.T @ x).astype(np.int64)       # exact: S <= 10^4 < 2^53
+
+
+@pytest.mark.parametrize("rel", sorted(r for r in MT if r.endswith(".csv")))
+def test_mt_product_path_matches_published(gpu_available, rel):
+    """legacy_probabilities(inst, 10^4, 0, rng="mt"): the alloc equals the reference's published
+    column bit for bit; pairs equal X^T X of the same MT panels (host); found_panels exact."""
+    A = pkg("analysis")
+    L = pkg("legacy")
+    g = MT[rel]
+    inst = _inst(g["instance"], g["k"])
+    alloc, found, hist = A.legacy_probabilities(inst, g["S"], 0, rng="mt")
+    assert [alloc[i] for i in range(len(alloc))] == g["selection_probability"]
+    enc = pkg().encode(inst.categories, inst.agents)
+    random.seed(0)
+    st = np.zeros(3, np.uint64)
+    _, panels, attempts = L.mt_draw(enc, g["k"], g["S"], stats=st)
+    want = _host_pairs(panels, enc.n)
+    iu = np.triu_indices(enc.n, 1)
+    assert hist.upper().tolist() == (want[iu] / g["S"]).tolist()
+    assert len(found) == len(np.unique(panels, axis=0))
+    assert set(found) == {tuple(int(p) for p in np.flatnonzero(
+        np.unpackbits(r.view(np.uint8), bitorder="little")[:enc.n])) for r in panels}
+    assert A.LAST_RUN_STATS == {"attempts": int(attempts.sum()), "selection_errors": int(st[1]),
+                                "rejections": int(st[2])}
+    assert int(st[0]) == int(attempts.sum())
+
+
+@pytest.mark.parametrize("name", ["couples_panel_from_twenty_people_no_constraints_2", "example_small_20"])
+def test_mt_product_path_seed1_unique(gpu_available, name):
+    """seed 1 (run_legacy_or_retrieve(resample=True)): the device's exact distinct count of the MT
+    panels equals the reference's published unique-panel count (analysis/*_statistics.txt)."""
+    A = pkg("analysis")
+    k = int(name.rsplit("_", 1)[1])
+    _, found, _ = A.legacy_probabilities(_inst(name, k), 10000, 1, rng="mt")
+    assert len(found) == MT["statistics_seed1"][name]["unique"]
+
+
+@pytest.mark.parametrize("W,S", [(1, 1), (1, 5000), (4, 777), (27, 4096), (128, 1000), (256, 300)])
+def test_panel_hash_async_matches_host_mirror(gpu_available, W, S):
+    """csa_panel_hash_async (the hash of host-drawn MT panels) == distributed.panel_hashes, on random
+    rows plus repeated and all-zero rows."""
+    import torch
+    N = pkg("_native")
+    D = pkg("distributed")
+    rng = np.random.default_rng(W * 7919 + S)
+    p = rng.integers(0, 2 ** 63, size=(S, W), dtype=np.uint64) ^ rng.integers(0, 2, size=(S, W), dtype=np.uint64)
+    if S > 4:
+        p[1] = p[0]
+        p[2] = 0
+    d = torch.from_numpy(p.view(np.int64).reshape(-1).copy()).cuda()
+    h = torch.zeros(2 * S, dtype=torch.int64, device="cuda")
+    N.check(N.lib().csa_panel_hash_async(N.ptr(d), S, W, N.ptr(h), None))
+    torch.cuda.synchronize()
+    got = h.cpu().numpy().view(np.uint64).reshape(S, 2)
+    assert np.array_equal(got, D.panel_hashes(p))
+
+
+_LOAD_CHILD = r"""
+import os, pickle, sys
+import numpy as np
+sys.path.insert(0, %(repo)r)
+with open(%(path)r, "rb") as fh:
+    alloc, found, hist = pickle.load(fh)
+assert "torch" not in sys.modules, "unpickling needed torch"
+ids = sorted(alloc)
+np.save(%(alloc)r, np.array([alloc[i] for i in ids]))
+np.save(%(upper)r, hist.upper())
+np.save(%(found)r, np.array(sorted(found), dtype=np.int64).reshape(len(found), -1))
+print(len(found))
+"""
+
+
+@pytest.mark.parametrize("name,k,S,seed,rng", [("example_small_20", 20, 3000, 4, "philox"),
+                                               ("couples_panel_from_twenty_people_no_constraints_2", 2, 5000, 1,
+                                                "philox"),
+                                               ("example_small_20", 20, 2000, 0, "mt")])
+def test_returned_tuple_pickles_without_gpu(gpu_available, tmp_path, name, k, S, seed, rng):
+    """pickle.dumps(legacy_probabilities(...)) as run_legacy_or_retrieve does (analysis.py:290),
+    pickle.load in a child process with every GPU hidden: alloc, found_panels and the pair
+    histogram are equal to the originals."""
+    A = pkg("analysis")
+    alloc, found, hist = A.legacy_probabilities(_inst(name, k), S, seed, rng=rng)
+    path = tmp_path / "legacy.pickle"
+    with open(path, "wb") as fh:
+        pickle.dump((alloc, found, hist), fh)
+    files = {key: str(tmp_path / (key + ".npy")) for key in ("alloc", "upper", "found")}
+    env = dict(os.environ, HIP_VISIBLE_DEVICES="-1", CUDA_VISIBLE_DEVICES="-1", ROCR_VISIBLE_DEVICES="-1")
+    out = subprocess.run([sys.executable, "-c", _LOAD_CHILD % dict(repo=REPO, path=str(path), **files)], env=env,
+                         capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stderr
+    assert int(out.stdout.strip()) == len(found)
+    assert np.load(files["alloc"]).tolist() == [alloc[i] for i in sorted(alloc)]
+    assert np.array_equal(np.load(files["upper"]), hist.upper())
+    assert [tuple(r) for r in np.load(files["found"]).tolist()] == sorted(found)
+
+
+@pytest.mark.parametrize("case", ["pathological_5_s0", "rejecty_6_s3", "sf_e_tight_110_s1", "couples_s0"])
+def test_draw_stats_match_reference(gpu_available, case):
+    """csa_instance_draw_stats after a csa_legacy_sample of a golden's panels: attempts,
+    SelectionError restarts and min-quota rejections equal the reference's own split."""
+    A = pkg("analysis")
+    g = golden(case)
+    inst = _inst(g["instance"], g["k"])
+    enc = pkg().encode(inst.categories, inst.agents)
+    raw = A.legacy_sample_raw(enc, g["k"], g["S"], g["seed"], want_pairs=False, want_panels=False)
+    assert raw.stats == {"attempts": sum(g["attempts"]), "selection_errors": sum(g["selection_errors"]),
+                         "rejections": sum(g["rejections"])}
+    alloc, _, _ = A.legacy_probabilities(inst, g["S"], g["seed"])
+    assert A.LAST_RUN_STATS == raw.stats
+
+
+def test_exchange_local_distinct_beyond_partitioned_path(gpu_available):
+    """csa_exchange_pack_async on 8192 x 2048 + 4096 entries (the partitioned dedupe's limit + 1
+    block): the global-table fallback lists exactly one index per distinct panel."""
+    import torch
+    N = pkg("_native")
+    D = pkg("distributed")
+    n = 8192 * 2048 + 4096
+    rng = np.random.default_rng(5)
+    base = rng.integers(0, 2 ** 63, size=n // 3, dtype=np.uint64)
+    p = base[rng.integers(0, len(base), size=n)].reshape(n, 1)     # many duplicates
+    want = len(np.unique(p))
+    dp = torch.from_numpy(p.view(np.int64).reshape(-1).copy()).cuda()
+    dh = torch.empty(2 * n, dtype=torch.int64, device="cuda")
+    N.check(N.lib().csa_panel_hash_async(N.ptr(dp), n, 1, N.ptr(dh), None))
+    status = torch.zeros(4, dtype=torch.int32, device="cuda")
+    rows, cnt = D.local_distinct_rows(dh, dp, n, 1, status)
+    assert cnt == want
+    got = np.sort(rows.cpu().numpy().view(np.uint64))
+    assert np.array_equal(got, np.unique(p))
+    assert int(status[0].item()) == 0
+
+
+def _bench(args, env_extra):
+    env = dict(os.environ, **env_extra)
+    out = subprocess.run([sys.executable, os.path.join(REPO, "bench.py")] + args, env=env, capture_output=True,
+                         text=True, timeout=400, cwd=REPO)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out.stdout[-2000:]
+    return json.loads(lines[0])
+
+
+@pytest.mark.timeout(600)
+def test_bench_self_launch_two_ranks_equals_one(gpu_available):
+    """`python bench.py --gpus 2` (no launcher; gloo rehearsal with both ranks on this GPU) starts its
+    own two ranks and prints one line with n_gpus 2 whose checks equal the N = 1 run over the same
+    global panels; the one-process multi-device leg (csa_legacy_sample_devices over the ranks'
+    devices) equals the rank-sharded result."""
+    common = ["--steps", "3", "--warmup", "1", "--no-cpu-baseline", "--no-api", "--iso-steps", "0"]
+    two = _bench(["--gpus", "2", "--panels", "20000"] + common, {"CSA_BENCH_BACKEND": "gloo"})
+    one = _bench(["--gpus", "1", "--panels", "40000"] + common, {})
+    assert two["n_gpus"] == 2 and one["n_gpus"] == 1
+    for key in ("last_step_unique", "last_step_count_sum", "last_step_pair_sum"):
+        assert two["checks"][key] == one["checks"][key]
+    assert two["checks"]["sample_devices"]["equal_to_rank_sharded"] is True
+    st = two["draw_stats"]
+    assert st["attempts"] == st["panels"] + st["selection_errors"] + st["rejections"]

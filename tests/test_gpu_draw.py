@@ -53,12 +53,19 @@ def test_draw_layouts_match_oracle(gpu_available, draw_group, group, name, k, S,
     inst = P.read_instance(*inst_paths(name), k)
     enc = P.encode(inst.categories, inst.agents)
     begin = 987654321
+    A = pkg("analysis")
+    A.draw_stats(enc, reset=True)
     panels, attempts = _sample(enc, k, S, seed, begin)
+    stats = A.draw_stats(enc)
     o = oracle_read(*inst_paths(name), k)
-    rc, opanels, oatt, _ = coracle.draw(o, k, seed, begin, S)
+    rejects = np.zeros(S, np.uint32)
+    rc, opanels, oatt, _ = coracle.draw(o, k, seed, begin, S, rejects=rejects)
     assert rc == 0
     assert np.array_equal(attempts, oatt)
     assert np.array_equal(panels, opanels)
+    # the kernel's restart counters (csa_instance_draw_stats) split like the oracle's
+    assert stats == {"attempts": int(oatt.sum()), "rejections": int(rejects.sum()),
+                     "selection_errors": int(oatt.sum()) - S - int(rejects.sum())}
 
 
 def _weird_instance():

@@ -430,6 +430,8 @@ def _dist_worker(rank, world, port, out_dir, name, k, S, seed):
         inst = pkg().read_instance(*inst_paths(name), k)
         alloc, found, hist = A.legacy_probabilities(inst, S, seed)      # world > 1: sharded
         if rank == world - 1:
+            np.save(os.path.join(out_dir, "unique_last.npy"), np.array([len(found)]))
+        if rank == 0:           # found_panels iterate on rank 0 (the ranks' distinct panels gathered)
             np.save(os.path.join(out_dir, "alloc.npy"), np.array([alloc[i] for i in range(len(alloc))]))
             np.save(os.path.join(out_dir, "upper.npy"), hist.upper())
             np.save(os.path.join(out_dir, "unique.npy"), np.array([len(found)]))
@@ -457,6 +459,7 @@ def test_legacy_probabilities_distributed_gloo(gpu_available, tmp_path, name, k,
     assert np.load(tmp_path / "alloc.npy").tolist() == [alloc[i] for i in range(len(alloc))]
     assert np.array_equal(np.load(tmp_path / "upper.npy"), hist.upper())
     assert int(np.load(tmp_path / "unique.npy")[0]) == len(found)
+    assert int(np.load(tmp_path / "unique_last.npy")[0]) == len(found)
     assert np.load(tmp_path / "found.npy").tolist() == [list(p) for p in sorted(found)]
 
 

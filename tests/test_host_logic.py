@@ -228,3 +228,32 @@ def test_encode_cached_revalidates():
     del agents[0]
     e3 = I.encode_cached(cats, agents)
     assert e3 is not e2 and e3.n == 199
+
+
+def test_result_tuple_pickles_host_only():
+    """PanelSet / PairHistogram pickle as host data (analysis.py:284-290 dumps the returned tuple):
+    the distinct panels travel as packed rows, the histogram as its divided matrix."""
+    A = pkg("analysis")
+    rng = np.random.default_rng(3)
+    n, S = 70, 500
+    panels = np.zeros((S, 2), np.uint64)
+    for i in range(S):
+        for p in rng.choice(n, size=5, replace=False):
+            panels[i, p >> 6] |= np.uint64(1) << np.uint64(p & 63)
+    panels[1] = panels[0]                      # a duplicate
+    ids = list(range(100, 100 + n))            # agent ids are not bit positions
+    want = {tuple(ids[p] for p in range(n) if (int(r[p >> 6]) >> (p & 63)) & 1) for r in panels}
+    ps = A.PanelSet(len(want), panels, n, ids)
+    counts = np.zeros((n, n), np.int64)
+    counts[np.triu_indices(n, 1)] = rng.integers(0, 9, size=n * (n - 1) // 2)
+    hist = A.PairHistogram(n, counts=counts)
+    hist.turn_into_probabilities_by_dividing_all_elements_by_given_number(S)
+    ps2, hist2 = pickle.loads(pickle.dumps((ps, hist)))
+    assert len(ps2) == len(want) and set(ps2) == want
+    assert ps2.rows().shape == (len(want), 2)
+    assert np.array_equal(hist2.upper(), counts[np.triu_indices(n, 1)] / S)
+    assert set(pickle.loads(pickle.dumps(ps2))) == want       # a materialised set pickles too
+    empty = pickle.loads(pickle.dumps(A.PanelSet(7, None, n, ids)))
+    assert len(empty) == 7
+    with pytest.raises(RuntimeError):
+        iter(empty)

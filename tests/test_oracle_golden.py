@@ -27,21 +27,25 @@ def _load(g):
 def test_c_oracle_matches_reference(case):
     g = golden(case)
     inst = _load(g)
-    rc, panels, attempts, picks = coracle.draw(inst, g["k"], g["seed"], 0, g["S"], want_picks=True)
+    rejects = np.zeros(g["S"], np.uint32)
+    rc, panels, attempts, picks = coracle.draw(inst, g["k"], g["seed"], 0, g["S"], want_picks=True, rejects=rejects)
     assert rc == 0
     n = inst.n
     assert _sha(panels) == g["panels_sha256"]
     assert attempts.tolist() == g["attempts"]
+    # restarts split as the reference raised them: SelectionErrors vs min-quota rejections
+    assert rejects.tolist() == g["rejections"]
+    assert (attempts - 1 - rejects).tolist() == g["selection_errors"]
     assert coracle.counts(panels, n).tolist() == g["counts"]
     assert coracle.unique(panels, n) == g["unique"]
     assert picks[: len(g["first_picks"])].tolist() == g["first_picks"]
-    if n <= 2000:
-        pr = coracle.pairs(panels, n)
-        up = pr[np.triu_indices(n, 1)]
-        assert _sha(up) == g["pair_upper_sha256"]
-        assert int(up.sum()) == g["pair_upper_sum"]
-        # derived probabilities: the reference's own float64 pair values
-        assert _sha(up / g["S"]) == g["pair_prob_sha256"]
+    # pairs at every n, synthetic8192_200_s0 included (200 reference panels, 33.5 M pairs)
+    pr = coracle.pairs(panels, n)
+    up = pr[np.triu_indices(n, 1)]
+    assert _sha(up) == g["pair_upper_sha256"]
+    assert int(up.sum()) == g["pair_upper_sum"]
+    # derived probabilities: the reference's own float64 pair values
+    assert _sha(up / g["S"]) == g["pair_prob_sha256"]
 
 
 @pytest.mark.parametrize("case", ["couples_s0", "couples_s1", "pathological_5_s0", "rejecty_6_s3",

@@ -52,7 +52,7 @@ CASES = [
     ("sf_e_tight_110_s1", "sf_e_tight_110", 110, 200, 1),
     ("pathological_5_s0", "pathological_5", 5, 2000, 0),
     ("rejecty_6_s3", "rejecty_6", 6, 2000, 3),
-    ("synthetic8192_200_s0", "synthetic8192_200", 200, 6, 0),
+    ("synthetic8192_200_s0", "synthetic8192_200", 200, 200, 0),
 ]
 
 
@@ -79,6 +79,7 @@ class PhiloxHarness:
         self.legacy, self.analysis, self.seed = legacy, analysis, seed
         self.panel, self.attempt, self.step, self.word = -1, -1, 0, None
         self.attempts, self.picks = [], []
+        self.selection_errors = []     # per panel: attempts that raised SelectionError (legacy.py:34-36)
 
     def __enter__(self):
         lg, an = self.legacy, self.analysis
@@ -90,6 +91,7 @@ class PhiloxHarness:
         def legacy_find(*a, **kw):
             h.panel += 1
             h.attempt = -1
+            h.selection_errors.append(0)
             out = orig_find(*a, **kw)
             h.attempts.append(h.attempt + 1)
             h.picks.append(list(out))
@@ -98,7 +100,11 @@ class PhiloxHarness:
         def find_random_sample_legacy(*a, **kw):
             h.attempt += 1
             h.step = 0
-            return orig_draw(*a, **kw)
+            try:
+                return orig_draw(*a, **kw)
+            except lg.SelectionError:
+                h.selection_errors[-1] += 1   # analysis.py:152-153 restarts; the rest are rejections
+                raise
 
         def find_max_ratio_cat(*a, **kw):
             h.word = legacy_word(h.seed, h.panel, h.attempt, h.step)
@@ -162,6 +168,10 @@ def run_case(legacy, analysis, case, inst_dir, k, S, seed):
         "counts": counts.tolist(),
         "unique": len(found),
         "attempts": h.attempts,
+        # attempts - 1 = SelectionError restarts (analysis.py:152-153) + min-quota rejections
+        # (the "Rejected" prints, analysis.py:155-159), split per panel
+        "selection_errors": h.selection_errors,
+        "rejections": [a - 1 - e for a, e in zip(h.attempts, h.selection_errors)],
         "panels_sha256": sha(pack(panels, n)),
         "pair_upper_sha256": sha(upper.astype(np.int64)),
         "pair_upper_sum": int(upper.sum()),
