@@ -69,6 +69,8 @@ def parse():
                          "stream (one pick-list buffer per panel buffer)")
     ap.add_argument("--iso-steps", type=int, default=2,
                     help="serial steps after the timed region that measure each kernel alone (not in `value`)")
+    ap.add_argument("--exchange", default="keys", choices=("keys", "bitmask"),
+                    help="N > 1: distinct panels travel as 24-byte keys (default) or with their bitmasks")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target duration of each CPU-baseline leg")
     ap.add_argument("--no-api", action="store_true", help="skip the legacy_probabilities end-to-end leg")
@@ -302,7 +304,10 @@ def main():
     split = pipe.split_draw and args.pack_on != "fused"   # separate pick-list draw + pack kernels
     W = enc.W
     # distinct-panel exchange buffers (fixed-capacity owner segments: no host sync per step)
-    xchg = Dd.PanelExchange(S, W, world, dev) if world > 1 else None
+    # 24-byte keys (hash + global panel index; hash matches re-drawn on the owner) unless
+    # --exchange bitmask
+    xchg = Dd.PanelExchange(S, W, world, dev, redraw=(enc.handle, k, args.seed, 0) if args.exchange == "keys"
+                            else None) if world > 1 else None
 
     overlap = not args.no_overlap
     nb = max(args.bufs, 2) if overlap else 1
@@ -381,7 +386,7 @@ def main():
             with torch.cuda.stream(stream):   # collectives order on the current stream
                 last["unique"] = Dd.combine(pipe.counts, pipe.pairs, pipe.hashes[: 2 * S], pipe.panels[: S * W], W,
                                             exchange=xchg, stream=stream, pair_bound=S * world,
-                                            status=pipe.status)[2]
+                                            status=pipe.status, panel_begin=(j * world + rank) * S)[2]
         if e:
             e[4].record(stream)
             rec[j].update({"xt_count": (e[0], e[1]), "pairs": (e[1], e[2]), "unique": (e[2], e[3]),
@@ -511,7 +516,8 @@ def main():
                                  "note": "ops = S*n*(n+1) (upper triangle incl. diagonal of 2*S*n^2); "
                                          "ms includes the partial-block reduce kernel"}
     if world > 1:
-        kernels["exchange"] = {"ms": stage_ms["exchange"]}
+        kernels["exchange"] = {"ms": stage_ms["exchange"], "form": args.exchange,
+                               "bytes_sent_per_rank": xchg.bytes_sent()}
     for key, st in (("draw", "draw"), ("pack", "pack"), ("xt_count", "xt_count"), ("unique", "unique"),
                     ("pairs_mfma", "pairs"), ("exchange", "exchange")):
         if key in kernels:

@@ -134,6 +134,10 @@ struct DrawArgs {
     // draw statistics (csa_instance_draw_stats): [0] SelectionError restarts, [1] min-quota
     // rejections; one fire-and-forget atomic per restart (null: not counted)
     unsigned long long *stats;
+    // draw_kernel GENERAL only: draw the panels panel_list[i] (i < min(n_panels, *n_panels_dev)) into
+    // row i instead of panel_begin + i (the multi-GPU owner's re-draw of hash-match candidates)
+    const uint64_t *panel_list;
+    const unsigned long long *n_panels_dev;
     int32_t *sel_out, *rem_out;
     uint64_t *present_out;
 };
@@ -269,6 +273,9 @@ __global__ __launch_bounds__(draw_threads(FPL, WPL), draw_occupancy(FPL, WPL)) v
     const int F = A.F, W = A.W, k = A.k;
     const int KR = (k + 3) & ~3;
     const int groups_wg = blockDim.x / G;
+    // an index-list re-draw sized for its worst case: workgroups past the list's length (usually
+    // all of them) leave before loading the feature rows
+    if (GENERAL && A.n_panels_dev && (uint64_t)blockIdx.x * groups_wg >= (uint64_t)*A.n_panels_dev) return;
     uint64_t *fm = smem;
     uint32_t *rng_all = reinterpret_cast<uint32_t *>(smem + FR * Ls);
     uint64_t *dscr_all = reinterpret_cast<uint64_t *>(rng_all + (size_t)groups_wg * KR);
@@ -309,7 +316,8 @@ __global__ __launch_bounds__(draw_threads(FPL, WPL), draw_occupancy(FPL, WPL)) v
     uint64_t i = (uint64_t)blockIdx.x * groups_wg + gwg;
     uint32_t a = 0;
     int s = 0;
-    bool active = i < A.n_panels;
+    const uint64_t n_panels = (GENERAL && A.n_panels_dev) ? min(A.n_panels, (uint64_t)*A.n_panels_dev) : A.n_panels;
+    bool active = i < n_panels;
     const bool single = GENERAL && A.single;
     const uint32_t max_att = single ? 1u : A.max_attempts;
     const uint32_t key0 = (uint32_t)A.seed, key1 = (uint32_t)(A.seed >> 32);
@@ -317,7 +325,7 @@ __global__ __launch_bounds__(draw_threads(FPL, WPL), draw_occupancy(FPL, WPL)) v
 
     while (__ballot(active) != 0ull) {
         if (active) {
-            const uint64_t panel = A.panel_begin + i;
+            const uint64_t panel = (GENERAL && A.panel_list) ? A.panel_list[i] : A.panel_begin + i;
             if (s == 0) {  // start of an attempt (legacy_find's fresh deepcopy, analysis.py:147-148)
 #pragma unroll
                 for (int j = 0; j < FPL; ++j) {
@@ -553,7 +561,7 @@ __global__ __launch_bounds__(draw_threads(FPL, WPL), draw_occupancy(FPL, WPL)) v
                     i += n_groups;
                     a = 0;
                     s = 0;
-                    active = i < A.n_panels;
+                    active = i < n_panels;
                     if (active && __hip_atomic_load(&A.status[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u)
                         active = false;
                 }
@@ -647,7 +655,11 @@ __global__ __launch_bounds__(kXtThreads) void xt_count_kernel(const uint64_t *__
             uint64_t x = w < CW ? tile[lane * Wp + w] : 0ull;
             x = wave_transpose64(x, lane);
             const int p = 64 * w + lane;
-            if (xt) xt[b * (uint64_t)npad + p0 + p] = x;
+            if (xt) {  // two 32-bit planes per panel block: panels 64b..64b+31, then 64b+32..64b+63
+                uint32_t *x32 = reinterpret_cast<uint32_t *>(xt) + 2 * b * (uint64_t)npad + p0 + p;
+                x32[0] = (uint32_t)x;
+                x32[npad] = (uint32_t)(x >> 32);
+            }
             if (p < np) cnt[p] += (uint32_t)__popcll(x);
         }
     }
@@ -765,7 +777,8 @@ __global__ __launch_bounds__(kPairThreads) void pair_mfma_kernel(const uint64_t 
 #pragma unroll
         for (int j = 0; j < KB; ++j) {  // blocks past the split's end stage as zero words (no contribution)
             const uint64_t b = kb0 + s * KB + j;
-            nw[j] = b < kb1 ? xt[b * (uint64_t)npad + src] : 0ull;
+            const uint32_t *x32 = reinterpret_cast<const uint32_t *>(xt) + 2 * b * (uint64_t)npad + src;
+            nw[j] = b < kb1 ? ((uint64_t)x32[0] | ((uint64_t)x32[npad] << 32)) : 0ull;
         }
     };
     if (nst) {
@@ -877,6 +890,332 @@ __global__ __launch_bounds__(256) void pair_reduce_kernel(const int32_t *__restr
     // no zero-fill of the n x n output before a fresh batch
     if (overwrite) pairs[(size_t)row * n + col] = acc;
     else if (acc) pairs[(size_t)row * n + col] += acc;
+}
+
+// ---- pair_fp4_tile_kernel: X^T X with the tiles grouped by XCD (fp4 engine) ----------------
+// One persistent 256-thread workgroup per CU (4 waves, one per SIMD, 256 accumulator registers
+// each): wave (wr, wc) owns rows 128 wr .. and columns 128 wc .. of a 256 x 256 output tile, 16
+// MFMAs per 64-panel block from 4 A and 4 B fragments (3 VALU of fragment expansion per MFMA,
+// against 4.25 in pair_mfma_kernel's 128 x 64 wave tile).  XT arrives by LDS-DMA
+// (global_load_lds_dwordx4, one 1 KiB piece per wave per block: A plane 0 / 1, B plane 0 / 1 --
+// the planes make every fragment read conflict-free) into a ring of kP2Depth blocks, one raw
+// barrier per block, the fragments of block j + 1 read while block j's MFMAs run.
+// Work (PairMap): the upper-triangular tiles in locality order (bands of 4 tile rows, columns left
+// to right) are cut into 8 contiguous chunks, one per XCD (workgroup g runs on XCD g mod 8), so the
+// 32 workgroups of an XCD stream few XT strips through its L2 together; an XCD's chunk of T tiles
+// runs as floor(T / 32) rounds of whole tiles (f32 accumulators, exact below 2^24 panels, stored
+// straight into the int64 output); the T mod 32 leftover tiles of all XCDs are pooled and cut into
+// 256 / (their number) k-pieces each, one per workgroup, written as int32 partial tiles that
+// pair_reduce2_kernel sums -- no round runs part-empty (n = 8192: 2 rounds + 16 tiles x 16 pieces;
+// sf_e, n = 1727: 28 tiles x 9 pieces).
+constexpr int kP2Threads = 256;
+constexpr int kP2Depth = 8;      // LDS ring slots = blocks in flight (4 KiB each)
+constexpr int kP2Xcds = 8;
+constexpr uint64_t kP2MaxBlocks = ((1ull << 24) - 1) / 64;  // whole-tile items stay exact in f32
+
+struct PairMap {
+    int nbt, ntri, P;   // tiles per side, upper-triangle tiles, workgroups per XCD
+    uint64_t nblk;      // 64-panel blocks
+    // tile at locality-order index idx
+    __host__ __device__ void tile_at(int idx, int &bi, int &bj) const {
+        int r0 = 0;
+        for (;;) {
+            const int hb = nbt - r0 < 4 ? nbt - r0 : 4;
+            const int cnt = hb * (hb + 1) / 2 + (nbt - r0 - hb) * hb;
+            if (idx < cnt) break;
+            idx -= cnt;
+            r0 += 4;
+        }
+        const int hb = nbt - r0 < 4 ? nbt - r0 : 4;
+        const int tri = hb * (hb + 1) / 2;
+        if (idx < tri) {  // the band's diagonal corner: column r0 + c holds rows r0 .. r0 + c
+            int c = 0;
+            while (idx > c) {
+                idx -= c + 1;
+                ++c;
+            }
+            bj = r0 + c;
+            bi = r0 + idx;
+        } else {
+            idx -= tri;
+            bj = r0 + hb + idx / hb;
+            bi = r0 + idx % hb;
+        }
+    }
+    __host__ __device__ void xcd_chunk(int x, int &t0, int &tx) const {
+        t0 = (int)((int64_t)ntri * x / kP2Xcds);
+        tx = (int)((int64_t)ntri * (x + 1) / kP2Xcds) - t0;
+    }
+    // leftover tiles (the last tx mod P of each XCD chunk) pooled over the XCDs: their number, the
+    // k-pieces per tile (every workgroup takes at most one piece), and the tile of pooled index l
+    __host__ __device__ int leftovers() const {
+        int tl = 0;
+        for (int x = 0; x < kP2Xcds; ++x) {
+            int t0, tx;
+            xcd_chunk(x, t0, tx);
+            tl += tx % P;
+        }
+        return tl;
+    }
+    __host__ __device__ int pieces(int tl) const { return tl ? (kP2Xcds * P) / tl : 0; }
+    __host__ __device__ int leftover_tile(int l) const {
+        for (int x = 0;; ++x) {
+            int t0, tx;
+            xcd_chunk(x, t0, tx);
+            const int lx = tx % P;
+            if (l < lx || x == kP2Xcds - 1) return t0 + (tx - lx) + l;
+            l -= lx;
+        }
+    }
+};
+
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef const __attribute__((address_space(1))) void gbl_void_t;
+
+// MODE 0: one barrier per block; 1: one per two blocks; 2: one per block with the fragments of block
+// j + 1 expanded while block j's MFMAs run (raw words two blocks ahead)
+template <int MODE>
+__global__ __launch_bounds__(kP2Threads, 1) void pair_fp4_tile_kernel(const uint32_t *__restrict__ xt, int n,
+                                                                       int npad, PairMap M,
+                                                                       int64_t *__restrict__ pairs,
+                                                                       int32_t *__restrict__ part, int overwrite) {
+    __shared__ uint32_t ring[kP2Depth][4][kPairBlock];  // slot: A plane 0, A plane 1, B plane 0, B plane 1
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int wr = wave >> 1, wc = wave & 1, r32 = lane & 31, h = lane >> 5;
+    const int x = (int)blockIdx.x % kP2Xcds, w = (int)blockIdx.x / kP2Xcds;
+    int t0, tx;
+    M.xcd_chunk(x, t0, tx);
+    // whole tiles of this XCD's chunk, round r = tiles t0 + r P .. (its 32 workgroups together), then
+    // at most one k-piece of a pooled leftover tile (piece g of tile g / sp for workgroup g)
+    const int F = tx / M.P, tl = M.leftovers(), sp = M.pieces(tl), g = (int)blockIdx.x;
+    const int items = F + (g < tl * sp ? 1 : 0);
+    for (int it = 0; it < items; ++it) {
+        int idx, slot = -1;
+        uint64_t kb0 = 0, kb1 = M.nblk;
+        if (it < F) {
+            idx = t0 + it * M.P + w;
+        } else {
+            const int q = g % sp;
+            idx = M.leftover_tile(g / sp);
+            kb0 = M.nblk * (uint64_t)q / (uint64_t)sp;
+            kb1 = M.nblk * (uint64_t)(q + 1) / (uint64_t)sp;
+            slot = g;
+        }
+        int bi, bj;
+        M.tile_at(idx, bi, bj);
+        const int I0 = bi * kPairBlock, J0 = bj * kPairBlock;
+        v16f acc[4][4];
+#pragma unroll
+        for (int a = 0; a < 4; ++a)
+#pragma unroll
+            for (int b = 0; b < 4; ++b)
+#pragma unroll
+                for (int v = 0; v < 16; ++v) acc[a][b][v] = 0.0f;
+        // this wave's DMA piece of every block: plane (wave & 1) of the A (waves 0, 1) or B strip
+        const uint32_t *gsrc = xt + (uint64_t)(wave & 1) * npad + (wave < 2 ? I0 : J0) + 4 * lane;
+        asm volatile("" : "+v"(gsrc));
+        const int nb = (int)(kb1 - kb0);  // <= kP2MaxBlocks
+        const uint32_t *gblk = gsrc + 2 * kb0 * (uint64_t)npad;
+        const uint64_t bstride = 2 * (uint64_t)npad;
+        // every DMA of the previous item has landed (ring slots are refilled below) and every wave is
+        // done reading the ring
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        // Branch-free pipeline: every step issues exactly one DMA per wave (past the last block it
+        // re-loads the last block into a slot nobody reads again), so the counted waits are constant:
+        // before step j, D + j pieces were issued and block j + 1 is the (j + 2)-th -> vmcnt(D - 2).
+        auto dma = [&](int blk, int slot) {
+            __builtin_amdgcn_global_load_lds((gbl_void_t *)(gblk + (uint64_t)min(blk, nb - 1) * bstride),
+                                             (lds_void_t *)&ring[slot][wave][0], 16, 0, 0);
+        };
+        auto compute = [&](const uint32_t(&ca)[4], const uint32_t(&cb)[4]) {
+            v8i fa[4], fb[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                fa[q] = f4_frag_a(ca[q]);
+                fb[q] = f4_frag_b(cb[q]);
+            }
+#pragma unroll
+            for (int a = 0; a < 4; ++a)
+#pragma unroll
+                for (int b = 0; b < 4; ++b)
+                    acc[a][b] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(fa[a], fb[b], acc[a][b], 4, 4, 0,
+                                                                                0x7F7F7F7F, 0, 0x7F7F7F7F);
+        };
+        static_assert((kP2Depth & (kP2Depth - 1)) == 0 && kP2Depth >= 4, "ring slots: power of two >= 4");
+        auto read_blk = [&](int blk, uint32_t(&na)[4], uint32_t(&nbw)[4]) {
+            const int sl = blk & (kP2Depth - 1);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                na[q] = ring[sl][h][128 * wr + 32 * q + r32];
+                nbw[q] = ring[sl][2 + h][128 * wc + 32 * q + r32];
+            }
+        };
+        if constexpr (MODE == 0) {
+            // one barrier per block: block j + 1 readable (this wave's piece by the counted wait, the
+            // others' by the barrier, which also retires every wave's reads of block j, whose slot
+            // then takes block j + D), its words read while block j's MFMAs run.  Before step j,
+            // D + j pieces were issued and block j + 1 is the (j + 2)-th -> vmcnt(D - 2).
+            auto step = [&](int j, const uint32_t(&ca)[4], const uint32_t(&cb)[4], uint32_t(&na)[4],
+                            uint32_t(&nbw)[4]) {
+                __builtin_amdgcn_sched_barrier(0);  // the previous block's MFMAs stay ahead of this barrier
+                asm volatile("s_waitcnt lgkmcnt(0)\n\ts_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(kP2Depth - 2) : "memory");
+                dma(j + kP2Depth, j & (kP2Depth - 1));
+                read_blk(j + 1, na, nbw);
+                compute(ca, cb);
+            };
+            if (nb > 0) {
+#pragma unroll
+                for (int j = 0; j < kP2Depth; ++j) dma(j, j);
+                asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(kP2Depth - 1) : "memory");
+                uint32_t ra[4], rb[4], sa[4], sb[4];
+                read_blk(0, ra, rb);
+                int j = 0;
+                for (; j + 2 < nb; j += 2) {
+                    step(j, ra, rb, sa, sb);
+                    step(j + 1, sa, sb, ra, rb);
+                }
+                if (j + 1 < nb) {
+                    step(j, ra, rb, sa, sb);
+                    __builtin_amdgcn_sched_barrier(0);
+                    compute(sa, sb);
+                } else {
+                    compute(ra, rb);
+                }
+            }
+        } else if constexpr (MODE == 2) {
+            // Raw words two blocks ahead, fragments one block ahead: step j waits for block j + 2
+            // (this wave's piece: vmcnt; the others': the barrier, which also retires every read of
+            // block j, whose slot takes block j + D), reads block j + 2's words, expands block j + 1's
+            // (VALU interleaved with block j's MFMAs, so the next step's first MFMA does not wait on
+            // its fragments) and runs block j's MFMAs.  Before step j, D + j pieces were issued and
+            // block j + 2 is the (j + 3)-th -> vmcnt(D - 3).
+            auto expand = [&](const uint32_t(&ca)[4], const uint32_t(&cb)[4], v8i(&fa)[4], v8i(&fb)[4]) {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    fa[q] = f4_frag_a(ca[q]);
+                    fb[q] = f4_frag_b(cb[q]);
+                }
+            };
+            auto mfma = [&](const v8i(&fa)[4], const v8i(&fb)[4]) {
+#pragma unroll
+                for (int a = 0; a < 4; ++a)
+#pragma unroll
+                    for (int b = 0; b < 4; ++b)
+                        acc[a][b] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(fa[a], fb[b], acc[a][b], 4, 4, 0,
+                                                                                    0x7F7F7F7F, 0, 0x7F7F7F7F);
+            };
+            if (nb > 0) {
+#pragma unroll
+                for (int j = 0; j < kP2Depth; ++j) dma(j, j);
+                asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(kP2Depth - 2) : "memory");
+                uint32_t r0a[4], r0b[4], r1a[4], r1b[4];
+                v8i f0a[4], f0b[4], f1a[4], f1b[4];
+                read_blk(0, r0a, r0b);
+                read_blk(1, r1a, r1b);
+                expand(r0a, r0b, f0a, f0b);
+                auto step = [&](int j, const v8i(&fca)[4], const v8i(&fcb)[4], const uint32_t(&rna)[4],
+                                const uint32_t(&rnb)[4], v8i(&fna)[4], v8i(&fnb)[4], uint32_t(&rwa)[4],
+                                uint32_t(&rwb)[4]) {
+                    __builtin_amdgcn_sched_barrier(0);
+                    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(kP2Depth - 3) : "memory");
+                    dma(j + kP2Depth, j & (kP2Depth - 1));
+                    read_blk(j + 2, rwa, rwb);
+                    expand(rna, rnb, fna, fnb);
+                    mfma(fca, fcb);
+                };
+                int j = 0;
+                for (; j + 2 <= nb; j += 2) {
+                    step(j, f0a, f0b, r1a, r1b, f1a, f1b, r0a, r0b);
+                    step(j + 1, f1a, f1b, r0a, r0b, f0a, f0b, r1a, r1b);
+                }
+                if (j < nb) step(j, f0a, f0b, r1a, r1b, f1a, f1b, r0a, r0b);
+            }
+        } else {
+            // one barrier per two blocks: at even j it makes blocks j + 1 and j + 2 readable and retires
+            // every read of blocks j - 1 and j, whose slots take blocks j + D - 1 and j + D.  The
+            // prologue issues D - 1 pieces, each even step two more: before even step j, D - 1 + j were
+            // issued and block j + 2 is the (j + 3)-th -> vmcnt(D - 4).  Odd steps only read and compute.
+            if (nb > 0) {
+#pragma unroll
+                for (int j = 0; j < kP2Depth - 1; ++j) dma(j, j);
+                asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(kP2Depth - 2) : "memory");
+                uint32_t ra[4], rb[4], sa[4], sb[4];
+                read_blk(0, ra, rb);
+                auto even = [&](int j) {  // computes block j (ra, rb), reads block j + 1 into (sa, sb)
+                    __builtin_amdgcn_sched_barrier(0);
+                    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(kP2Depth - 4) : "memory");
+                    dma(j + kP2Depth - 1, (j - 1) & (kP2Depth - 1));
+                    dma(j + kP2Depth, j & (kP2Depth - 1));
+                    read_blk(j + 1, sa, sb);
+                    compute(ra, rb);
+                };
+                int j = 0;
+                for (; j + 2 < nb; j += 2) {
+                    even(j);
+                    __builtin_amdgcn_sched_barrier(0);
+                    read_blk(j + 2, ra, rb);  // landed by the even barrier
+                    compute(sa, sb);
+                }
+                if (j + 1 < nb) {
+                    even(j);
+                    __builtin_amdgcn_sched_barrier(0);
+                    compute(sa, sb);
+                } else {
+                    compute(ra, rb);
+                }
+            }
+        }
+        // C/D layout: col = lane & 31, row = (v & 3) + 8 (v >> 2) + 4 (lane >> 5).  The lane offsets
+        // are laundered through an empty asm so that the compiler does not hoist the 256 store
+        // addresses of the epilogue out of the item loop (they spilled, and the spill traffic
+        // shares vmcnt with the LDS-DMA pipeline)
+        int rloc = 128 * wr + 4 * h, cloc = 128 * wc + r32;
+        asm volatile("" : "+v"(rloc), "+v"(cloc));
+        if (slot >= 0) {
+            int32_t *dst = part + (size_t)slot * kPairBlock * kPairBlock;
+#pragma unroll
+            for (int a = 0; a < 4; ++a)
+#pragma unroll
+                for (int b = 0; b < 4; ++b)
+#pragma unroll
+                    for (int v = 0; v < 16; ++v)
+                        dst[(rloc + 32 * a + (v & 3) + 8 * (v >> 2)) * kPairBlock + cloc + 32 * b] = (int)acc[a][b][v];
+        } else {
+#pragma unroll
+            for (int a = 0; a < 4; ++a)
+#pragma unroll
+                for (int b = 0; b < 4; ++b) {
+                    const int col = J0 + cloc + 32 * b;
+#pragma unroll
+                    for (int v = 0; v < 16; ++v) {
+                        const int row = I0 + rloc + 32 * a + (v & 3) + 8 * (v >> 2);
+                        if (row < n && col < n) {
+                            int64_t *o = pairs + (uint64_t)row * n + col;
+                            const int64_t val = (int64_t)acc[a][b][v];
+                            *o = overwrite ? val : *o + val;
+                        }
+                    }
+                }
+        }
+    }
+}
+
+// Sums the k-pieces of the pooled leftover tiles of pair_fp4_tile_kernel (piece q of leftover tile l
+// in partial slot l * sp + q) into the int64 output: block (row, l) = row `row` of leftover tile l.
+__global__ __launch_bounds__(kPairBlock) void pair_reduce2_kernel(const int32_t *__restrict__ part, int n, PairMap M,
+                                                                 int64_t *__restrict__ pairs, int overwrite) {
+    const int l = (int)blockIdx.y, sp = M.pieces(M.leftovers());
+    int bi, bj;
+    M.tile_at(M.leftover_tile(l), bi, bj);
+    const int r = (int)blockIdx.x, c = (int)threadIdx.x;
+    const int row = bi * kPairBlock + r, col = bj * kPairBlock + c;
+    if (row >= n || col >= n) return;
+    const int32_t *p = part + (size_t)(l * sp) * kPairBlock * kPairBlock + r * kPairBlock + c;
+    int64_t acc = 0;
+    for (int q = 0; q < sp; ++q) acc += p[(size_t)q * kPairBlock * kPairBlock];
+    int64_t *o = pairs + (uint64_t)row * n + col;
+    *o = overwrite ? acc : *o + acc;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1181,6 +1520,125 @@ __global__ __launch_bounds__(kXbThreads) void exchange_bucket_kernel(
         const uint64_t d = dst_row[r];
         if (d != ~0ull) send_panels[d * W + w] = panels[(uint64_t)src_row[r] * W + w];
     }
+}
+
+// ---- the 24-byte exchange (keys instead of bitmasks) ---------------------------------------
+// A panel is a pure function of (seed, global panel index) in the Philox stream, so a rank sends,
+// per local distinct panel, its 128-bit hash and global index (24 B instead of 16 + 8W B); the
+// owner counts distinct hashes and re-draws only the entries whose hash matched an earlier one
+// (their bitmasks decide: a duplicate, or -- never seen in practice -- a 128-bit collision, whose
+// mismatched members are then counted exactly by bitmask).
+__global__ __launch_bounds__(kXbThreads) void exchange_keys_kernel(
+    const uint64_t *__restrict__ hashes, const uint32_t *__restrict__ rep, const unsigned long long *__restrict__ rep_count,
+    uint64_t panel_begin, uint32_t world, uint64_t capacity, uint64_t *__restrict__ send_keys,
+    unsigned long long *__restrict__ send_counts, uint32_t *__restrict__ status) {
+    __shared__ uint32_t hist[kMaxWorld];
+    __shared__ unsigned long long rbase[kMaxWorld];
+    const uint64_t m = *rep_count;
+    const uint64_t e0 = (uint64_t)blockIdx.x * kXbThreads;
+    if (e0 >= m) return;  // whole workgroup
+    for (uint32_t w = threadIdx.x; w < world; w += blockDim.x) hist[w] = 0;
+    __syncthreads();
+    const uint64_t e = e0 + threadIdx.x;
+    const bool valid = e < m;
+    uint32_t i = 0, owner = 0, local = 0;
+    uint64_t h1 = 0, h2 = 0;
+    if (valid) {
+        i = rep[e];
+        h1 = hashes[2 * (uint64_t)i];
+        h2 = hashes[2 * (uint64_t)i + 1];
+        owner = (uint32_t)(h1 % world);
+        local = atomicAdd(&hist[owner], 1u);
+    }
+    __syncthreads();
+    for (uint32_t w = threadIdx.x; w < world; w += blockDim.x)
+        rbase[w] = hist[w] ? atomicAdd(&send_counts[w], (unsigned long long)hist[w]) : 0ull;
+    __syncthreads();
+    if (valid) {
+        const uint64_t pos = rbase[owner] + local;
+        if (pos < capacity) {
+            uint64_t *d = send_keys + 3 * ((uint64_t)owner * capacity + pos);
+            d[0] = h1;
+            d[1] = h2;
+            d[2] = panel_begin + i;
+        } else {
+            raise_status(status, CSA_E_UNSUPPORTED, kExchangeOverflow);
+        }
+    }
+}
+
+// Owner, pass 1: distinct 128-bit hashes among the valid entries of the segmented keys (entry e
+// valid iff e % seg_cap < seg_counts[e / seg_cap]); an entry whose hash equals an earlier-inserted
+// entry's goes to the re-draw list as the pair (its panel index, that entry's panel index).
+__global__ void key_unique_kernel(const uint64_t *__restrict__ keys, uint64_t total, uint32_t seg_cap,
+                                  const uint64_t *__restrict__ seg_counts, unsigned long long *__restrict__ table,
+                                  uint64_t mask, unsigned long long *__restrict__ unique, uint64_t *__restrict__ list,
+                                  unsigned long long *__restrict__ list_len, uint64_t list_cap,
+                                  uint32_t *__restrict__ status) {
+    const uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    bool inserted = false;
+    if (e < total && uq_valid(e, seg_cap, seg_counts)) {
+        const uint64_t h1 = keys[3 * e], h2 = keys[3 * e + 1];
+        uint64_t slot = (h1 ^ (h2 >> 29)) & mask;
+        for (uint64_t probe = 0; probe <= mask; ++probe) {
+            const unsigned long long v = atomicCAS(table + slot, 0ull, (unsigned long long)(e + 1));
+            if (v == 0ull) {
+                inserted = true;
+                break;
+            }
+            const uint64_t j = v - 1;
+            if (keys[3 * j] == h1 && keys[3 * j + 1] == h2) {  // same hash: re-draw both to compare
+                const unsigned long long c = atomicAdd(list_len, 2ull);
+                if (c + 2 <= 2 * list_cap) {
+                    list[c] = keys[3 * e + 2];
+                    list[c + 1] = keys[3 * j + 2];
+                } else {
+                    raise_status(status, CSA_E_UNSUPPORTED, kExchangeOverflow);
+                }
+                break;
+            }
+            slot = (slot + 1) & mask;
+        }
+    }
+    const uint64_t b = __ballot(inserted);
+    if ((threadIdx.x & 63) == 0 && b) atomicAdd(unique, (unsigned long long)__popcll(b));
+}
+
+// Owner, pass 2 (after the re-draw of the list into rows): a candidate whose bitmask differs from
+// its hash partner's is a different panel behind a 128-bit hash collision; those are counted
+// exactly among themselves (table2, keyed by their own hash, bitmask comparison).
+__global__ void key_verify_kernel(const uint64_t *__restrict__ rows, int W, const unsigned long long *__restrict__ list_len,
+                                  unsigned long long *__restrict__ table2, uint64_t mask2,
+                                  unsigned long long *__restrict__ unique) {
+    const uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    bool added = false;
+    if (2 * c < *list_len) {
+        const uint64_t *x = rows + 2 * c * (uint64_t)W, *y = x + W;
+        bool same = true;
+        for (int w = 0; w < W && same; ++w) same = x[w] == y[w];
+        if (!same) {
+            uint64_t h1 = 0, h2 = 0;
+            for (int w = 0; w < W; ++w) {
+                h1 += fmix_a(x[w] ^ ((uint64_t)w * 0x9E3779B97F4A7C15ull));
+                h2 += fmix_b(x[w] + ((uint64_t)w + 1) * 0xD6E8FEB86659FD93ull);
+            }
+            uint64_t slot = (h1 ^ (h2 >> 29)) & mask2;
+            for (uint64_t probe = 0; probe <= mask2; ++probe) {
+                const unsigned long long v = atomicCAS(table2 + slot, 0ull, (unsigned long long)(c + 1));
+                if (v == 0ull) {
+                    added = true;
+                    break;
+                }
+                const uint64_t *z = rows + 2 * (v - 1) * (uint64_t)W;
+                bool eq = true;
+                for (int w = 0; w < W && eq; ++w) eq = x[w] == z[w];
+                if (eq) break;
+                slot = (slot + 1) & mask2;
+            }
+        }
+    }
+    const uint64_t b = __ballot(added);
+    if ((threadIdx.x & 63) == 0 && b) atomicAdd(unique, (unsigned long long)__popcll(b));
 }
 
 // Multi-GPU pair exchange: the upper triangle (incl. the diagonal) of the n x n int64 pair counts
@@ -1546,7 +2004,8 @@ int launch_draw(const csa_instance *I, int32_t k, uint64_t seed, uint64_t panel_
                 uint32_t max_attempts, uint32_t attempt_base, int single, uint64_t *d_panels,
                 uint64_t *d_hashes, uint32_t *d_attempts, int32_t *d_picks, uint32_t *d_status,
                 int32_t *d_sel_out, int32_t *d_rem_out, uint64_t *d_present_out, hipStream_t stream,
-                uint16_t *d_picks_ext = nullptr) {
+                uint16_t *d_picks_ext = nullptr, const uint64_t *d_panel_list = nullptr,
+                const unsigned long long *d_list_len = nullptr) {
     int rc = check_k(I, k);
     if (rc) return rc;
     if ((!d_panels && !d_picks_ext) || !d_status) return fail(CSA_E_INVALID, "d_panels and d_status are required");
@@ -1573,7 +2032,7 @@ int launch_draw(const csa_instance *I, int32_t k, uint64_t seed, uint64_t panel_
         return CSA_OK;
     }
     DrawConfig cfg;
-    int rc2 = pick_draw_config(I, single || d_picks || d_sel_out || d_present_out, cfg);
+    int rc2 = pick_draw_config(I, single || d_picks || d_sel_out || d_present_out || d_panel_list, cfg);
     if (rc2) return rc2;
     DrawArgs A;
     A.featmask = I->d_featmask;
@@ -1602,7 +2061,9 @@ int launch_draw(const csa_instance *I, int32_t k, uint64_t seed, uint64_t panel_
     A.picks16 = nullptr;
     A.status = d_status;
     // legacy_find-semantics draws are counted; single attempts (csa_legacy_attempt) are not
-    A.stats = single ? nullptr : I->d_stats;
+    A.stats = (single || d_panel_list) ? nullptr : I->d_stats;
+    A.panel_list = d_panel_list;   // an index list: draw_kernel GENERAL (pick_draw_config above)
+    A.n_panels_dev = d_list_len;
     A.sel_out = d_sel_out;
     A.rem_out = d_rem_out;
     A.present_out = d_present_out;
@@ -1643,7 +2104,7 @@ int launch_draw(const csa_instance *I, int32_t k, uint64_t seed, uint64_t panel_
     void *args[] = {&A};
     HIPCHK(hipLaunchKernel(cfg.fn, dim3((unsigned)std::max<uint64_t>(1, grid)), dim3(threads), args, lds, stream));
     HIPCHK(hipGetLastError());
-    if (!single) M->panels_drawn += n_panels;
+    if (!single && !d_panel_list) M->panels_drawn += n_panels;  // (index-list re-draws are not new panels)
     if (cfg.picks() && !d_picks_ext) {  // pick lists -> packed panels (+ hashes)
         if (!fused && (rc = launch_pack(A.picks16, n_panels, k, I->W, d_panels, d_hashes, stream))) return rc;
         HIPCHK(hipEventRecord(M->picks_done, stream));
@@ -2156,11 +2617,48 @@ int pair_plan(int32_t n, uint64_t n_blocks, uint32_t engine, PairPlan &p) {
     p.nsplit = (int)ns;
     return CSA_OK;
 }
+// pair_fp4_tile_kernel's plan (fp4 engine, whole-tile items exact in f32, CUs in 8 XCD groups):
+// false when it does not apply (pair_mfma_kernel then runs).  It is taken when the triangle has at
+// least one tile per CU (n >= ~5.7k): there pair_mfma_kernel's one-split launch ends in a part-empty
+// round (n = 8192: 528 blocks = 2.06 rounds; 16.0 vs 10.3 ms alone, 29.3 vs 31.2 M panels/s end to
+// end).  Below it the split kernel stays: alone the two are level, but its 2 waves/SIMD leave room
+// for a draw wave beside it on a CU, and inside the pipelined step that is worth more (sf_e 263.4 vs
+// 257.7 M panels/s, example_large_200 300.2 vs 289.4; tools/gpu_ab_env.sh).
+// CSA_PAIR_KERNEL=1 forces pair_mfma_kernel, =2 this kernel wherever it applies.
+struct Pair2Plan {
+    PairMap M;
+    int grid = 0, lmax = 0;  // persistent workgroups; leftover tiles (pooled over the XCDs)
+};
+
+bool pair2_plan(int32_t n, uint64_t n_blocks, uint32_t engine, Pair2Plan &q) {
+    if (engine != CSA_PAIR_FP4 || n_blocks == 0 || n_blocks > kP2MaxBlocks) return false;
+    const char *e = getenv("CSA_PAIR_KERNEL");
+    const int force = e ? atoi(e) : 0;
+    if (force == 1) return false;
+    int cus = 256, dev = 0;
+    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (cus < kP2Xcds || cus % kP2Xcds) return false;
+    q.M.nbt = csa_xt_pad(n) / kPairBlock;
+    q.M.ntri = q.M.nbt * (q.M.nbt + 1) / 2;
+    q.M.P = cus / kP2Xcds;
+    q.M.nblk = n_blocks;
+    q.grid = cus;
+    q.lmax = q.M.leftovers();  // pooled leftover tiles (each in pieces(lmax) int32 partial slots)
+    return force == 2 || q.M.ntri >= cus;
+}
+
+uint64_t pair2_scratch_bytes(const Pair2Plan &q) {
+    return q.lmax ? (uint64_t)q.lmax * q.M.pieces(q.lmax) * kPairBlock * kPairBlock * sizeof(int32_t) : 0;
+}
 }  // namespace
 
 uint64_t csa_pair_scratch_bytes(int32_t n, uint64_t n_blocks, uint32_t engine) {
+    engine &= ~CSA_PAIR_OVERWRITE;
+    if (n <= 0 || n_blocks == 0) return 0;
+    Pair2Plan q;
+    if (pair2_plan(n, n_blocks, engine, q)) return std::max<uint64_t>(pair2_scratch_bytes(q), 4);
     PairPlan p;
-    if (n <= 0 || n_blocks == 0 || pair_plan(n, n_blocks, engine & ~CSA_PAIR_OVERWRITE, p)) return 0;
+    if (pair_plan(n, n_blocks, engine, p)) return 0;
     return (uint64_t)p.ntri * p.nsplit * kPairBlock * kPairBlock * sizeof(int32_t);
 }
 
@@ -2173,6 +2671,31 @@ int csa_pair_counts_ex_async(const uint64_t *d_xt, uint64_t n_blocks, int32_t n,
     if (overwrite && (n_blocks == 0 || !d_scratch))  // no reduce pass to store every element
         HIPCHK(hipMemsetAsync(d_pairs, 0, (size_t)n * n * sizeof(int64_t), st));
     if (n_blocks == 0) return CSA_OK;
+    Pair2Plan q;
+    if (d_scratch && pair2_plan(n, n_blocks, engine, q)) {
+        if (scratch_bytes < pair2_scratch_bytes(q))
+            return fail(CSA_E_INVALID, "pairs: scratch of %llu B < csa_pair_scratch_bytes = %llu B",
+                        (unsigned long long)scratch_bytes, (unsigned long long)pair2_scratch_bytes(q));
+        int32_t *part = static_cast<int32_t *>(d_scratch);
+        const uint32_t *xt32 = reinterpret_cast<const uint32_t *>(d_xt);
+        const int npad = csa_xt_pad(n), ow = overwrite ? 1 : 0;
+        // CSA_P2_MODE=0|1|2 selects the pipeline variant (A/B); default 2
+        const char *pm = getenv("CSA_P2_MODE");
+        const int mode = pm ? atoi(pm) : 2;
+        const void *fn = mode == 0   ? reinterpret_cast<const void *>(&pair_fp4_tile_kernel<0>)
+                         : mode == 1 ? reinterpret_cast<const void *>(&pair_fp4_tile_kernel<1>)
+                                     : reinterpret_cast<const void *>(&pair_fp4_tile_kernel<2>);
+        PairMap M = q.M;
+        void *args[] = {(void *)&xt32, &n, (void *)&npad, &M, &d_pairs, &part, (void *)&ow};
+        HIPCHK(hipLaunchKernel(fn, dim3(q.grid), dim3(kP2Threads), args, 0, st));
+        HIPCHK(hipGetLastError());
+        if (q.lmax) {
+            hipLaunchKernelGGL(pair_reduce2_kernel, dim3(kPairBlock, q.lmax), dim3(kPairBlock), 0, st,
+                               (const int32_t *)part, n, q.M, d_pairs, ow);
+            HIPCHK(hipGetLastError());
+        }
+        return CSA_OK;
+    }
     PairPlan p;
     int rc = pair_plan(n, n_blocks, engine, p);
     if (rc) return rc;
@@ -2270,6 +2793,96 @@ int csa_exchange_pack_async(const uint64_t *d_hashes, const uint64_t *d_panels, 
     hipLaunchKernelGGL(exchange_bucket_kernel, dim3(grid), dim3(kXbThreads), 0, st, d_hashes, d_panels, W, rep,
                        rep_count, world, capacity, d_send_hashes, d_send_panels,
                        reinterpret_cast<unsigned long long *>(d_send_counts), d_status);
+    HIPCHK(hipGetLastError());
+    return CSA_OK;
+}
+
+int csa_exchange_keys_async(const uint64_t *d_hashes, const uint64_t *d_panels, uint64_t n_panels, int32_t W,
+                            uint64_t panel_begin, uint32_t world, uint64_t capacity, void *d_scratch,
+                            uint64_t scratch_bytes, uint64_t *d_send_keys, uint64_t *d_send_counts, uint32_t *d_status,
+                            void *stream) {
+    if (!d_hashes || !d_panels || W <= 0 || world == 0 || world > (uint32_t)kMaxWorld || capacity == 0 ||
+        !d_scratch || !d_send_keys || !d_send_counts || !d_status)
+        return fail(CSA_E_INVALID, "exchange keys: bad arguments");
+    if (n_panels >= (1ull << 31)) return fail(CSA_E_UNSUPPORTED, "exchange keys: n_panels >= 2^31 (u32 indices)");
+    if (scratch_bytes < csa_exchange_scratch_bytes(n_panels))
+        return fail(CSA_E_INVALID, "exchange keys: scratch_bytes < csa_exchange_scratch_bytes(n_panels)");
+    const hipStream_t st = (hipStream_t)stream;
+    unsigned long long *rep_count = reinterpret_cast<unsigned long long *>(d_scratch);
+    uint32_t *rep = reinterpret_cast<uint32_t *>(rep_count + 1);
+    uint32_t *part = rep + ((std::max<uint64_t>(n_panels, 1) + 1) & ~1ull);
+    HIPCHK(hipMemsetAsync(rep_count, 0, 8, st));
+    HIPCHK(hipMemsetAsync(d_send_counts, 0, (size_t)world * 8, st));
+    if (n_panels == 0) return CSA_OK;
+    UqPlan q;
+    uq_plan(n_panels, q);
+    if (q.fits) {
+        int rc = uq_partitioned(d_hashes, d_panels, n_panels, W, q, part, nullptr, d_status, 0, nullptr, rep, rep_count,
+                                st);
+        if (rc) return rc;
+    } else {
+        const uint64_t slots = pow2_at_least(std::max<uint64_t>(2 * n_panels, 64));
+        unsigned long long *table = reinterpret_cast<unsigned long long *>(part);
+        HIPCHK(hipMemsetAsync(table, 0, slots * 8, st));
+        hipLaunchKernelGGL(unique_kernel, dim3((unsigned)((n_panels + 255) / 256)), dim3(256), 0, st, d_hashes, d_panels,
+                           n_panels, W, table, slots - 1, nullptr, 0u, nullptr, rep, rep_count);
+        HIPCHK(hipGetLastError());
+    }
+    const unsigned grid = (unsigned)((n_panels + kXbThreads - 1) / kXbThreads);
+    hipLaunchKernelGGL(exchange_keys_kernel, dim3(grid), dim3(kXbThreads), 0, st, d_hashes, rep, rep_count, panel_begin,
+                       world, capacity, d_send_keys, reinterpret_cast<unsigned long long *>(d_send_counts), d_status);
+    HIPCHK(hipGetLastError());
+    return CSA_OK;
+}
+
+// owner scratch: table | list (2 n) | list_len | re-drawn rows (2 n x W) | table2
+static void unique_keys_layout(uint64_t n_keys, int32_t W, uint64_t &slots, uint64_t &slots2, uint64_t &words) {
+    const uint64_t n = std::max<uint64_t>(n_keys, 1);
+    slots = pow2_at_least(std::max<uint64_t>(2 * n, 64));
+    slots2 = slots;
+    words = slots + 2 * n + 1 + 2 * n * (uint64_t)std::max(W, 1) + slots2;
+}
+
+uint64_t csa_unique_keys_scratch_bytes(uint64_t n_keys, int32_t W) {
+    uint64_t slots, slots2, words;
+    unique_keys_layout(n_keys, W, slots, slots2, words);
+    return 8 * words;
+}
+
+int csa_unique_keys_async(const csa_instance *I, int32_t k, uint64_t seed, uint32_t max_attempts, const uint64_t *d_keys,
+                          uint32_t n_segments, uint64_t capacity, const uint64_t *d_seg_counts, void *d_scratch,
+                          uint64_t scratch_bytes, uint64_t *d_unique, uint32_t *d_status, void *stream) {
+    if (!I || !d_keys || !d_seg_counts || !d_scratch || !d_unique || !d_status || capacity == 0 ||
+        capacity > 0xFFFFFFFFull || n_segments == 0)
+        return fail(CSA_E_INVALID, "unique keys: bad arguments");
+    const uint64_t total = (uint64_t)n_segments * capacity;
+    const int W = I->W;
+    if (scratch_bytes < csa_unique_keys_scratch_bytes(total, W))
+        return fail(CSA_E_INVALID, "unique keys: scratch_bytes < csa_unique_keys_scratch_bytes");
+    uint64_t slots, slots2, words;
+    unique_keys_layout(total, W, slots, slots2, words);
+    uint64_t *base = static_cast<uint64_t *>(d_scratch);
+    unsigned long long *table = reinterpret_cast<unsigned long long *>(base);
+    uint64_t *list = base + slots;
+    unsigned long long *list_len = reinterpret_cast<unsigned long long *>(list + 2 * total);
+    uint64_t *rows = list + 2 * total + 1;
+    unsigned long long *table2 = reinterpret_cast<unsigned long long *>(rows + 2 * total * (uint64_t)W);
+    const hipStream_t st = (hipStream_t)stream;
+    HIPCHK(hipMemsetAsync(table, 0, slots * 8, st));
+    HIPCHK(hipMemsetAsync(list_len, 0, 8, st));
+    HIPCHK(hipMemsetAsync(table2, 0, slots2 * 8, st));
+    const unsigned grid = (unsigned)((total + 255) / 256);
+    hipLaunchKernelGGL(key_unique_kernel, dim3(grid), dim3(256), 0, st, d_keys, total, (uint32_t)capacity, d_seg_counts,
+                       table, slots - 1, reinterpret_cast<unsigned long long *>(d_unique), list, list_len, total,
+                       d_status);
+    HIPCHK(hipGetLastError());
+    // re-draw the listed panels (a persistent index-list draw: workgroups past the list leave at once)
+    int rc = launch_draw(I, k, seed, 0, 2 * total, max_attempts, 0, 0, rows, nullptr, nullptr, nullptr, d_status,
+                         nullptr, nullptr, nullptr, st, nullptr, list, list_len);
+    if (rc) return rc;
+    hipLaunchKernelGGL(key_verify_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, (const uint64_t *)rows,
+                       W, (const unsigned long long *)list_len, table2, slots2 - 1,
+                       reinterpret_cast<unsigned long long *>(d_unique));
     HIPCHK(hipGetLastError());
     return CSA_OK;
 }

@@ -187,33 +187,52 @@ def _all_to_all(out, inp):
 class PanelExchange:
     """The distinct-panel exchange of one rank, buffers sized once for n_local panels of W words.
 
-    ``run(hashes, panels, n, status, stream)`` returns this rank's owner count (a 1-element int64
-    tensor, device or host like the inputs); the caller all_reduces it.  Device inputs: no host
-    synchronisation (csa_exchange_pack_async -> three equal-split all_to_alls ->
-    csa_unique_segments_async), so a caller can enqueue the next steps behind it."""
+    ``run(hashes, panels, n, status, stream, panel_begin)`` returns this rank's owner count (a
+    1-element int64 tensor, device or host like the inputs); the caller all_reduces it.  Device
+    inputs: no host synchronisation, so a caller can enqueue the next steps behind it.
 
-    def __init__(self, n_local, W, world, device):
+    With ``redraw = (instance handle, k, seed, max_attempts)`` (the draw that made the panels, Philox
+    mode) the 24-byte exchange runs: keys (h1, h2, global panel index) instead of bitmasks
+    (csa_exchange_keys_async -> two equal-split all_to_alls -> csa_unique_keys_async, which re-draws
+    only the hash-matched entries to compare their bitmasks).  Without it, the bitmasks travel
+    (csa_exchange_pack_async -> three all_to_alls -> csa_unique_segments_async); host tensors always
+    take that form through its numpy mirrors."""
+
+    def __init__(self, n_local, W, world, device, redraw=None):
         import torch
         from . import _native as N
         self.W, self.world, self.device = int(W), int(world), device
         self.n_local = max(int(n_local), 1)
         self.cap = exchange_capacity(self.n_local, self.world)
         self.cuda = torch.device(device).type == "cuda"
+        self.redraw = redraw if self.cuda else None
         if not self.cuda:
             return
         i64 = torch.int64
         seg = self.world * self.cap
-        self.send_h = torch.empty(2 * seg, dtype=i64, device=device)
-        self.send_p = torch.empty(seg * self.W, dtype=i64, device=device)
-        self.send_c = torch.zeros(self.world, dtype=i64, device=device)
-        self.recv_h = torch.empty_like(self.send_h)
-        self.recv_p = torch.empty_like(self.send_p)
-        self.recv_c = torch.zeros_like(self.send_c)
         sb = int(N.lib().csa_exchange_scratch_bytes(self.n_local))
         self.scratch = torch.empty((sb + 7) // 8, dtype=i64, device=device)
+        self.send_c = torch.zeros(self.world, dtype=i64, device=device)
+        self.recv_c = torch.zeros_like(self.send_c)
+        self.unique = torch.zeros(1, dtype=i64, device=device)
+        if self.redraw is not None:
+            self.send_k = torch.empty(3 * seg, dtype=i64, device=device)
+            self.recv_k = torch.empty_like(self.send_k)
+            ob = int(N.lib().csa_unique_keys_scratch_bytes(seg, self.W))
+            self.owner_scratch = torch.empty((ob + 7) // 8, dtype=i64, device=device)
+            return
+        self.send_h = torch.empty(2 * seg, dtype=i64, device=device)
+        self.send_p = torch.empty(seg * self.W, dtype=i64, device=device)
+        self.recv_h = torch.empty_like(self.send_h)
+        self.recv_p = torch.empty_like(self.send_p)
         self.table = HashTable(seg, device)
 
-    def run(self, hashes, panels, n, status=None, stream=None):
+    def bytes_sent(self):
+        """Bytes this rank puts into the all_to_alls per run (segments of every owner, itself included)."""
+        per = 24 if self.redraw is not None else 16 + 8 * self.W
+        return self.world * self.cap * per + 8 * self.world
+
+    def run(self, hashes, panels, n, status=None, stream=None, panel_begin=0):
         import torch
         n = int(n)
         assert n <= self.n_local
@@ -233,6 +252,20 @@ class PanelExchange:
         st = stream or torch.cuda.current_stream(hashes.device)
         sp_ = ctypes.c_void_p(st.cuda_stream)
         L = N.lib()
+        if self.redraw is not None:
+            handle, k, seed, max_att = self.redraw
+            N.check(L.csa_exchange_keys_async(N.ptr(hashes), N.ptr(panels), n, self.W, int(panel_begin), self.world,
+                                              self.cap, N.ptr(self.scratch), self.scratch.numel() * 8,
+                                              N.ptr(self.send_k), N.ptr(self.send_c), N.ptr(status), sp_))
+            with torch.cuda.stream(st):
+                _all_to_all(self.recv_c, self.send_c)
+                _all_to_all(self.recv_k, self.send_k)
+                self.unique.zero_()
+            N.check(L.csa_unique_keys_async(handle, int(k), int(seed) & M64, int(max_att), N.ptr(self.recv_k),
+                                            self.world, self.cap, N.ptr(self.recv_c), N.ptr(self.owner_scratch),
+                                            self.owner_scratch.numel() * 8, N.ptr(self.unique), N.ptr(status), sp_))
+            with torch.cuda.stream(st):
+                return self.unique.clone()
         N.check(L.csa_exchange_pack_async(N.ptr(hashes), N.ptr(panels), n, self.W, self.world, self.cap,
                                           N.ptr(self.scratch), self.scratch.numel() * 8, N.ptr(self.send_h),
                                           N.ptr(self.send_p), N.ptr(self.send_c), N.ptr(status), sp_))
@@ -280,13 +313,15 @@ def _all_reduce(t, op=None):
         dist.all_reduce(t, op=op)
 
 
-def combine(counts, pairs, hashes, panels, W, exchange=None, stream=None, pair_bound=None, status=None):
+def combine(counts, pairs, hashes, panels, W, exchange=None, stream=None, pair_bound=None, status=None, redraw=None,
+            panel_begin=0):
     """Exchange steps for this rank; returns (counts, pairs, unique_tensor), all stream-ordered.
 
     counts int64[n], pairs int64[n*n] or None, hashes int64[2*S_local] and panels
-    int64[S_local*W] (this rank's panels).  Counts and pairs: all_reduce(SUM).  Distinct
-    panels: ``exchange`` (a PanelExchange, built here if None) sends the local distinct panels
-    to their owners, each owner counts exactly, all_reduce(SUM) of the counts.
+    int64[S_local*W] (this rank's panels, global indices from ``panel_begin``).  Counts and pairs:
+    all_reduce(SUM).  Distinct panels: ``exchange`` (a PanelExchange, built here if None, with
+    ``redraw`` for the 24-byte keys) sends the local distinct panels to their owners, each owner
+    counts exactly, all_reduce(SUM) of the counts.
     """
     import torch
     import torch.distributed as dist
@@ -295,11 +330,11 @@ def combine(counts, pairs, hashes, panels, W, exchange=None, stream=None, pair_b
         # every rank must size its segments alike (equal-split all_to_all): the largest shard's
         n_max = torch.tensor([n_local], dtype=torch.int64, device=hashes.device)
         _all_reduce(n_max, op=dist.ReduceOp.MAX)
-        exchange = PanelExchange(int(n_max.item()), W, dist.get_world_size(), hashes.device)
+        exchange = PanelExchange(int(n_max.item()), W, dist.get_world_size(), hashes.device, redraw=redraw)
     _all_reduce(counts)
     if pairs is not None:
         _all_reduce_pairs(pairs, pair_bound, stream)
-    u = exchange.run(hashes, panels, n_local, status=status, stream=stream)
+    u = exchange.run(hashes, panels, n_local, status=status, stream=stream, panel_begin=panel_begin)
     if u.is_cuda:
         with torch.cuda.stream(stream or torch.cuda.current_stream(u.device)):
             _all_reduce(u)
@@ -422,7 +457,8 @@ def legacy_probabilities_distributed(instance, iterations, random_seed, keep_pan
         pipe.pair_counts(local)
     _raise_together(pipe.status, pipe.stream)
     counts, pairs, u = combine(pipe.counts, pipe.pairs, pipe.hashes[: 2 * local], pipe.panels[: local * enc.W],
-                               enc.W, pair_bound=S, status=pipe.status)
+                               enc.W, pair_bound=S, status=pipe.status, redraw=(enc.handle, instance.k, random_seed, 0),
+                               panel_begin=begin)
     _raise_together(pipe.status, pipe.stream)
     stats = torch.tensor(list(A.draw_stats(enc).values()), dtype=torch.int64, device=pipe.counts.device)
     _all_reduce(stats)

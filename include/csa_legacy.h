@@ -217,16 +217,19 @@ int csa_panel_hash_async(const uint64_t *d_panels, uint64_t n_panels, int32_t W,
 int csa_draw_kernel_name(const csa_instance *inst, int32_t k, char *buf, uint64_t len);
 
 /* Bit-transpose + per-person count.  Panels (n_panels*W) -> d_xt, the
- * panel-indicator matrix transposed and packed: d_xt[b * n_pad + p] holds
- * bits of agent p for panels 64b..64b+63; n_pad = csa_xt_pad(n), blocks
- * b < ceil(n_panels/64).  d_counts (n int64) is ACCUMULATED (+=); d_xt may be
- * NULL (counts only). */
+ * panel-indicator matrix transposed and packed in two 32-bit planes per
+ * 64-panel block b (uint32 view): d_xt32[(2b + h) * n_pad + p] holds the bits
+ * of agent p for panels 64b + 32h .. 64b + 32h + 31 (bit j = panel
+ * 64b + 32h + j); n_pad = csa_xt_pad(n), blocks b < ceil(n_panels/64), i.e.
+ * ceil(n_panels/64) * n_pad uint64 of storage.  The planes let the MFMA kernel
+ * read every fragment bank-conflict-free.  d_counts (n int64) is ACCUMULATED
+ * (+=); d_xt may be NULL (counts only). */
 int32_t csa_xt_pad(int32_t n);
 int csa_transpose_count_async(const uint64_t *d_panels, uint64_t n_panels, int32_t n,
                               uint64_t *d_xt, int64_t *d_counts, void *stream);
 
-/* Pair counts X^T X on MFMA, upper-triangular 256x256 blocks split over panel
- * blocks (replaces PairHistogram.add_portfolio_of_panels_to_histogram,
+/* Pair counts X^T X on MFMA, upper-triangular 256x256 blocks (replaces
+ * PairHistogram.add_portfolio_of_panels_to_histogram,
  * analysis.py:90-95, summed over all panels).  d_xt as produced above
  * (n_blocks = ceil(n_panels/64)); d_pairs (n*n int64, row-major) is
  * ACCUMULATED (+=) for i <= j (lower triangle unspecified).  Exact for any
@@ -234,9 +237,12 @@ int csa_transpose_count_async(const uint64_t *d_panels, uint64_t n_panels, int32
  * engine: CSA_PAIR_FP4 = v_mfma_scale_f32_32x32x64_f8f6f4 on e2m1 0/1-products
  * (f32 accumulation, exact below 2^24 per split); CSA_PAIR_I8 =
  * v_mfma_i32_32x32x32_i8 (int32 accumulation).  With d_scratch (at least
- * csa_pair_scratch_bytes bytes of device memory) each split writes an int32
- * partial block and a reduce kernel sums them; with d_scratch == NULL the
- * splits add into d_pairs with int64 atomics.  csa_pair_counts_async =
+ * csa_pair_scratch_bytes bytes of device memory) the fp4 engine runs one
+ * persistent workgroup per CU with the tiles grouped by XCD (whole tiles stored
+ * directly, the leftover tiles as k-pieces summed by a reduce kernel; <= 2^24
+ * panels per call, else as below); otherwise each split of the panel blocks
+ * writes an int32 partial block that a reduce kernel sums, or, with d_scratch ==
+ * NULL, adds into d_pairs with int64 atomics.  csa_pair_counts_async =
  * engine FP4, no scratch.  engine | CSA_PAIR_OVERWRITE stores instead of
  * accumulating: on return d_pairs holds exactly this batch's counts for i <= j
  * (the reduce kernel writes every element of the upper-triangular blocks; without
@@ -293,6 +299,26 @@ int csa_exchange_pack_async(const uint64_t *d_hashes, const uint64_t *d_panels, 
                             uint32_t world, uint64_t capacity, void *d_scratch, uint64_t scratch_bytes,
                             uint64_t *d_send_hashes, uint64_t *d_send_panels, uint64_t *d_send_counts,
                             uint32_t *d_status, void *stream);
+
+/* The 24-byte distinct-panel exchange.  A panel is a pure function of (seed, global panel index) in
+ * the Philox stream, so instead of its bitmask each local distinct panel travels as a key
+ * (h1, h2, panel_begin + local index).  Send side (as csa_exchange_pack_async otherwise):
+ * d_send_keys uint64[world][capacity][3], scratch csa_exchange_scratch_bytes(n_panels).  Owner
+ * side: *d_unique += the exact number of distinct panels among the valid keys of n_segments
+ * segments of `capacity` keys (segment s holds d_seg_counts[s]): the distinct 128-bit hashes, plus
+ * -- every key whose hash matched an earlier key being re-drawn on inst (draw over an index list,
+ * Philox (k, seed, max_attempts) as the original draws) together with that key's panel -- the
+ * mismatched ones (128-bit hash collisions) counted exactly by bitmask.  d_scratch:
+ * csa_unique_keys_scratch_bytes(n_segments * capacity, W) bytes. */
+int csa_exchange_keys_async(const uint64_t *d_hashes, const uint64_t *d_panels, uint64_t n_panels, int32_t W,
+                            uint64_t panel_begin, uint32_t world, uint64_t capacity, void *d_scratch,
+                            uint64_t scratch_bytes, uint64_t *d_send_keys, uint64_t *d_send_counts,
+                            uint32_t *d_status, void *stream);
+uint64_t csa_unique_keys_scratch_bytes(uint64_t n_keys, int32_t W);
+int csa_unique_keys_async(const csa_instance *inst, int32_t k, uint64_t seed, uint32_t max_attempts,
+                          const uint64_t *d_keys, uint32_t n_segments, uint64_t capacity,
+                          const uint64_t *d_seg_counts, void *d_scratch, uint64_t scratch_bytes,
+                          uint64_t *d_unique, uint32_t *d_status, void *stream);
 
 /* Multi-GPU pair exchange: pack the upper triangle incl. the diagonal of the
  * n*n int64 pair counts row-major into n(n+1)/2 int32 (every count must be

@@ -1,10 +1,17 @@
 """GPU parity of the X^T X pair-count kernels (PairHistogram, analysis.py:68-98) through the C ABI.
 
 Both MFMA engines (fp4 e2m1 with f32 accumulation, int8 with int32
-accumulation) and both epilogues (int32 partial blocks + reduce kernel, int64
-atomics) against an exact CPU popcount restatement on the same packed
-transposed bits.  Bar: bit-exact.
+accumulation), both fp4 kernels (pair_fp4_tile_kernel, the default with scratch;
+pair_mfma_kernel, CSA_PAIR_KERNEL=1) and every epilogue (direct whole tiles,
+int32 partial blocks + reduce kernels, int64 atomics) against an exact CPU
+popcount restatement on the same transposed bits.  Bar: bit-exact.
+
+The XT operand (csa_transpose_count_async's layout) is two 32-bit planes per
+64-panel block: xt32[b][0][p] = panels 64b..64b+31 of agent p, xt32[b][1][p] =
+panels 64b+32..64b+63.  The tests build it from uint64 words w[b][p] (bit j =
+panel 64b+j) with _planes.
 """
+import os
 import numpy as np
 import pytest
 
@@ -24,12 +31,30 @@ def _cpu_pairs(xt, n, npad, rows=None):
     return np.rint(X.T @ X).astype(np.int64)                      # BLAS; exact below 2^53
 
 
+def _planes(w):
+    """uint64 words [nblk, npad] -> the XT plane layout (uint32 [nblk, 2, npad]); numpy or torch."""
+    if isinstance(w, np.ndarray):
+        nblk, npad = w.shape
+        return np.ascontiguousarray(w.view(np.uint32).reshape(nblk, npad, 2).transpose(0, 2, 1))
+    import torch
+    nblk, npad = w.shape
+    return w.contiguous().view(torch.int32).view(nblk, npad, 2).permute(0, 2, 1).contiguous()
+
+
+@pytest.fixture(params=["tile", "split"])
+def pair_kernel(request, monkeypatch):
+    """fp4 kernel: pair_fp4_tile_kernel (CSA_PAIR_KERNEL=2; the default from n ~ 5.7k on) or
+    pair_mfma_kernel (CSA_PAIR_KERNEL=1; the default below)."""
+    monkeypatch.setenv("CSA_PAIR_KERNEL", "1" if request.param == "split" else "2")
+    return request.param
+
+
 def _run(xt_np, n, engine, scratch, init=0):
     import torch
     N = pkg("_native")
     L = N.lib()
     nblk = xt_np.shape[0]
-    xt = torch.from_numpy(xt_np.view(np.int64).copy()).cuda()
+    xt = torch.from_numpy(_planes(xt_np).view(np.int64).copy()).cuda()
     pairs = torch.full((n * n,), init, dtype=torch.int64, device="cuda")
     sb = int(L.csa_pair_scratch_bytes(n, nblk, engine))
     scr = torch.empty((sb + 3) // 4, dtype=torch.int32, device="cuda") if scratch else None
@@ -41,7 +66,7 @@ def _run(xt_np, n, engine, scratch, init=0):
 
 @pytest.mark.parametrize("n,S", [(20, 10000), (200, 70000), (300, 6400), (1727, 20000), (2000, 3000)])
 @pytest.mark.parametrize("engine,scratch", [(0, True), (0, False), (1, True), (1, False)])
-def test_pair_engines_exact(gpu_available, n, S, engine, scratch):
+def test_pair_engines_exact(gpu_available, pair_kernel, n, S, engine, scratch):
     N = pkg("_native")
     npad = int(N.lib().csa_xt_pad(n))
     nblk = (S + 63) // 64
@@ -59,7 +84,7 @@ def test_pair_engines_exact(gpu_available, n, S, engine, scratch):
 
 @pytest.mark.parametrize("n,S", [(20, 1000), (1727, 20000)])
 @pytest.mark.parametrize("engine,scratch", [(0, True), (0, False), (1, True)])
-def test_pair_overwrite_ignores_prior_contents(gpu_available, n, S, engine, scratch):
+def test_pair_overwrite_ignores_prior_contents(gpu_available, pair_kernel, n, S, engine, scratch):
     """CSA_PAIR_OVERWRITE: the output holds exactly this batch's counts whatever it held before
     (bench.py skips the n*n zero-fill this way); the plain mode adds onto the prior contents."""
     N = pkg("_native")
@@ -97,7 +122,8 @@ def test_pair_fp4_exact_beyond_f32_range(gpu_available):
     sb = int(L.csa_pair_scratch_bytes(n, nblk, N.CSA_PAIR_FP4))
     assert sb >= 2 * 300 * 256 * 256 * 4       # the exactness guard forced >= 2 splits
     scr = torch.empty(sb // 4, dtype=torch.int32, device="cuda")
-    N.check(L.csa_pair_counts_ex_async(N.ptr(xt), nblk, n, N.ptr(pairs), N.CSA_PAIR_FP4, N.ptr(scr), sb, None))
+    x32 = _planes(xt)
+    N.check(L.csa_pair_counts_ex_async(N.ptr(x32), nblk, n, N.ptr(pairs), N.CSA_PAIR_FP4, N.ptr(scr), sb, None))
     torch.cuda.synchronize()
     P = pairs.view(n, n)
     c1 = int(_popcount64(xt[:, 1].cpu().numpy()))
@@ -109,7 +135,7 @@ def test_pair_fp4_exact_beyond_f32_range(gpu_available):
 
 
 @pytest.mark.parametrize("engine", [0, 1])
-def test_pairs_n8192_vs_torch_fp32(gpu_available, engine):
+def test_pairs_n8192_vs_torch_fp32(gpu_available, pair_kernel, engine):
     """BASELINE config 5 shape: n = 8192 (32 triangle rows of 256 x 256 blocks), S = 131072 panels of
     ~2.5 % density (k ~ 200), against a plain PyTorch fp32 X^T X on the device (rocBLAS; exact:
     every partial sum <= S < 2^24, and gfx950 has no reduced-precision fp32 GEMM mode)."""
@@ -129,7 +155,8 @@ def test_pairs_n8192_vs_torch_fp32(gpu_available, engine):
     pairs = torch.full((n * n,), -7, dtype=torch.int64, device="cuda")
     sb = int(L.csa_pair_scratch_bytes(n, nblk, engine))
     scr = torch.empty((sb + 3) // 4, dtype=torch.int32, device="cuda")
-    N.check(L.csa_pair_counts_ex_async(N.ptr(xt), nblk, n, N.ptr(pairs), engine | N.CSA_PAIR_OVERWRITE, N.ptr(scr),
+    x32 = _planes(xt)
+    N.check(L.csa_pair_counts_ex_async(N.ptr(x32), nblk, n, N.ptr(pairs), engine | N.CSA_PAIR_OVERWRITE, N.ptr(scr),
                                        sb, None))
     Xf = X.to(torch.float32)
     ref = (Xf.T @ Xf).to(torch.int64)
@@ -137,3 +164,22 @@ def test_pairs_n8192_vs_torch_fp32(gpu_available, engine):
     got = pairs.view(n, n)
     assert torch.equal(torch.triu(got), torch.triu(ref))
     assert int(ref[17, 17].item()) == S
+
+
+@pytest.mark.parametrize("n,nblk", [(20, 1), (20, 31), (257, 3), (1727, 40), (4100, 7), (8192, 33)])
+@pytest.mark.parametrize("overwrite", [True, False])
+def test_pair_tile_kernel_small_and_ragged(gpu_available, monkeypatch, n, nblk, overwrite):
+    """pair_fp4_tile_kernel edge cases: fewer panel blocks than k-pieces (empty pieces), one tile only
+    (n = 20: one XCD has work), XCD chunks with and without leftover tiles, n not a multiple of 256."""
+    monkeypatch.setenv("CSA_PAIR_KERNEL", "2")
+    N = pkg("_native")
+    npad = int(N.lib().csa_xt_pad(n))
+    rng = np.random.default_rng(n * 31 + nblk)
+    xt = rng.integers(0, 2 ** 64, size=(nblk, npad), dtype=np.uint64) & rng.integers(0, 2 ** 64, size=(nblk, npad),
+                                                                                     dtype=np.uint64)
+    xt[:, n:] = 0
+    ref = _cpu_pairs(xt, n, npad)
+    iu = np.triu_indices(n)
+    engine = N.CSA_PAIR_FP4 | (N.CSA_PAIR_OVERWRITE if overwrite else 0)
+    got = _run(xt, n, engine, True, init=-3)
+    assert np.array_equal(got[iu], ref[iu] + (0 if overwrite else -3))

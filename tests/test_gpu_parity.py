@@ -304,6 +304,85 @@ def test_exchange_exact_on_device(gpu_available, world):
             assert got == exp
 
 
+def _keys_exchange_on_device(enc, k, seed, h, p, W, world, shards, cap, status):
+    """The 24-byte exchange with `world` simulated ranks on one device: each sender packs keys
+    (csa_exchange_keys_async, global index = shard begin + local index), the all_to_all is done by
+    slicing, each owner counts (csa_unique_keys_async, re-drawing its hash-matched keys)."""
+    import torch
+    N = pkg("_native")
+    L = N.lib()
+    sends = []
+    for b, e in shards:
+        sk = torch.zeros(world * cap * 3, dtype=torch.int64, device="cuda")
+        sc = torch.zeros(world, dtype=torch.int64, device="cuda")
+        sb = int(L.csa_exchange_scratch_bytes(max(e - b, 1)))
+        scratch = torch.empty((sb + 7) // 8, dtype=torch.int64, device="cuda")
+        N.check(L.csa_exchange_keys_async(N.ptr(h[2 * b:]), N.ptr(p[b * W:]), e - b, W, b, world, cap, N.ptr(scratch),
+                                          scratch.numel() * 8, N.ptr(sk), N.ptr(sc), N.ptr(status), None))
+        sends.append((sk, sc))
+    torch.cuda.synchronize()
+    total = 0
+    ob = int(L.csa_unique_keys_scratch_bytes(world * cap, W))
+    scr = torch.empty((ob + 7) // 8, dtype=torch.int64, device="cuda")
+    for r in range(world):
+        rk = torch.cat([sk[r * cap * 3:(r + 1) * cap * 3] for sk, _ in sends])
+        rc = torch.stack([sc[r] for _, sc in sends])
+        u = torch.zeros(1, dtype=torch.int64, device="cuda")
+        N.check(L.csa_unique_keys_async(enc.handle, k, seed, 0, N.ptr(rk), world, cap, N.ptr(rc), N.ptr(scr), ob,
+                                        N.ptr(u), N.ptr(status), None))
+        torch.cuda.synchronize()
+        total += int(u.item())
+    return total, [(sk.cpu().numpy().view(np.uint64).reshape(world, cap, 3), sc.cpu().numpy()) for sk, sc in sends]
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 8])
+@pytest.mark.parametrize("case", ["couples", "forged", "forged_dups"])
+def test_exchange_keys_exact_on_device(gpu_available, world, case):
+    """The 24-byte exchange (keys = 128-bit hash + global panel index; the owner re-draws hash-matched
+    keys and compares bitmasks): the owners' counts sum to the exact distinct count -- duplicates
+    split across senders (couples: 100 distinct panels), a forged hash collision between two
+    different panels (counted twice), and a forged collision whose other panel is itself
+    duplicated on several ranks (still counted once)."""
+    import torch
+    A = pkg("analysis")
+    D = pkg("distributed")
+    name, k, S, seed = (("example_small_20", 20, 5000, 3) if case == "forged" else
+                        ("couples_panel_from_twenty_people_no_constraints_2", 2, 20000, 5))
+    inst, enc = _enc(name, k)
+    panels = A.legacy_sample_raw(enc, k, S, seed, want_pairs=False, want_panels=True).panels
+    W = panels.shape[1]
+    hashes = D.panel_hashes(panels)
+    want = coracle.unique(panels, enc.n)
+    if case == "forged":
+        assert want == S
+        assert not np.array_equal(panels[0], panels[1000])
+        hashes[1000] = hashes[0]
+    elif case == "forged_dups":
+        x = panels[0]
+        y = next(r for r in panels if not np.array_equal(r, x))
+        hy = D.panel_hashes(y[None])[0]
+        same_x = (panels == x).all(axis=1)
+        hashes[same_x] = hy                 # every copy of panel x now hashes like panel y
+        assert same_x.sum() > world and want == 100
+    h = torch.from_numpy(hashes.ravel().view(np.int64).copy()).cuda()
+    p = torch.from_numpy(panels.ravel().view(np.int64).copy()).cuda()
+    status = torch.zeros(4, dtype=torch.int32, device="cuda")
+    shards = [D.shard_range(S, world, r) for r in range(world)]
+    cap = D.exchange_capacity(max(e - b for b, e in shards), world)
+    total, host = _keys_exchange_on_device(enc, k, seed, h, p, W, world, shards, cap, status)
+    assert int(status[0].item()) == 0
+    assert total == want
+    # every sender's keys: one per local distinct panel, owner h1 % world, index inside its shard
+    for (b, e), (sk, sc) in zip(shards, host):
+        mh, mp, mc = D.segment_buckets(hashes[b:e], panels[b:e], world, cap)
+        assert sc.tolist() == mc.tolist()
+        for w in range(world):
+            keys = sk[w, : sc[w]]
+            assert ((keys[:, 2] >= b) & (keys[:, 2] < e)).all()
+            assert np.array_equal(hashes[keys[:, 2].astype(np.int64)], keys[:, :2])
+            assert sorted(map(tuple, panels[keys[:, 2].astype(np.int64)].tolist())) == sorted(map(tuple, mp[w, : mc[w]].tolist()))
+
+
 def test_exchange_overflow_raises(gpu_available):
     """A segment past its capacity is an error in the status block (never a silently short count)."""
     import torch
