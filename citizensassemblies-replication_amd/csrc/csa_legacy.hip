@@ -2071,7 +2071,9 @@ int launch_draw(const csa_instance *I, int32_t k, uint64_t seed, uint64_t panel_
     csa_instance *M = const_cast<csa_instance *>(I);  // the lane kernel's pick-list scratch
     if (d_picks_ext)
         A.picks16 = d_picks_ext;
-    else if (cfg.picks() && (rc = lane_picks(M, n_panels * (uint64_t)((k + 7) & ~7), stream, &A.picks16)))
+    // (the fused pack's chunked layout reserves whole workgroups of <= 256 panels)
+    else if (cfg.picks() && (rc = lane_picks(M, ((n_panels + 255) & ~255ull) * (uint64_t)((k + 7) & ~7), stream,
+                                             &A.picks16)))
         return rc;
     const int threads = cfg.lane   ? kLaneThreads
                         : cfg.solo ? kSoloThreads

@@ -1,9 +1,13 @@
 // VALU throughput per SIMD on gfx950 for the instruction classes of the draw kernels
-// (diagnostic; the roofline of draw_lane_kernel is its VALU issue rate).
+// (diagnostic; the roofline of the draw kernels is their VALU issue rate).
 //   hipcc --offload-arch=gfx950 -O3 -o tools/valu_rate tools/valu_rate.hip && tools/valu_rate
-// Each kernel runs 8 independent chains of N instructions per lane, 8 waves per SIMD (2048
-// workgroups of 256 threads on 256 CUs), so issue -- not latency -- bounds it.  Prints cycles per
-// wave-instruction per SIMD: 2 = one wave64 VALU every 2 cycles (SIMD-32), 4 = every 4 cycles.
+// Each kernel runs 8 independent chains of N instructions per lane, with 1, 2, 4 or 8 waves per
+// SIMD (256, 512, 1024, 2048 workgroups of 256 threads on 256 CUs: the dispatcher spreads a
+// workgroup's 4 waves over the CU's 4 SIMDs), so issue -- not latency -- bounds it once a SIMD holds
+// enough waves.  Prints cycles per wave-instruction per SIMD at the reported peak clock: 2 = one
+// wave64 VALU every 2 cycles (SIMD-32 at full rate), 4 = every 4 cycles.  Packed ops (v_pk_*) do two
+// 16- or 32-bit operations per lane per instruction: their rows say whether that doubles the work
+// per issue slot (same cycles as the scalar form) or not.
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdint>
@@ -15,42 +19,29 @@ constexpr int kIters = 4096;  // x 8 chains x 8 unrolled ops
         _Pragma("unroll") for (int c = 0; c < 8; ++c) { OP(v[c]); }                     \
     }
 
-__global__ __launch_bounds__(256) void k_add(uint32_t *out, uint32_t s) {
-    uint32_t v[8];
-    for (int c = 0; c < 8; ++c) v[c] = threadIdx.x + c;
+#define KERNEL_U32(NAME, OP)                                                            \
+    __global__ __launch_bounds__(256) void NAME(uint32_t *out, uint32_t s) {            \
+        uint32_t v[8];                                                                  \
+        for (int c = 0; c < 8; ++c) v[c] = threadIdx.x + c;                             \
+        CHAINS(OP)                                                                      \
+        uint32_t r = 0;                                                                 \
+        for (int c = 0; c < 8; ++c) r ^= v[c];                                          \
+        out[blockIdx.x * blockDim.x + threadIdx.x] = r;                                 \
+    }
+
 #define OPADD(x) asm volatile("v_add_u32 %0, %0, %1" : "+v"(x) : "s"(s))
-    CHAINS(OPADD)
-    uint32_t r = 0;
-    for (int c = 0; c < 8; ++c) r ^= v[c];
-    out[blockIdx.x * blockDim.x + threadIdx.x] = r;
-}
-__global__ __launch_bounds__(256) void k_bcnt(uint32_t *out, uint32_t s) {
-    uint32_t v[8];
-    for (int c = 0; c < 8; ++c) v[c] = threadIdx.x + c;
 #define OPBCNT(x) asm volatile("v_bcnt_u32_b32 %0, %0, %1" : "+v"(x) : "s"(s))
-    CHAINS(OPBCNT)
-    uint32_t r = 0;
-    for (int c = 0; c < 8; ++c) r ^= v[c];
-    out[blockIdx.x * blockDim.x + threadIdx.x] = r;
-}
-__global__ __launch_bounds__(256) void k_cndmask(uint32_t *out, uint32_t s) {
-    uint32_t v[8];
-    for (int c = 0; c < 8; ++c) v[c] = threadIdx.x + c;
 #define OPCND(x) asm volatile("v_cndmask_b32_e64 %0, %0, %1, vcc" : "+v"(x) : "v"(s))
-    CHAINS(OPCND)
-    uint32_t r = 0;
-    for (int c = 0; c < 8; ++c) r ^= v[c];
-    out[blockIdx.x * blockDim.x + threadIdx.x] = r;
-}
-__global__ __launch_bounds__(256) void k_mul24sdwa(uint32_t *out, uint32_t s) {
-    uint32_t v[8];
-    for (int c = 0; c < 8; ++c) v[c] = threadIdx.x + c;
 #define OPMUL(x) asm volatile("v_mul_i32_i24_sdwa %0, sext(%0), %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_1 src1_sel:WORD_0" : "+v"(x) : "v"(s))
-    CHAINS(OPMUL)
-    uint32_t r = 0;
-    for (int c = 0; c < 8; ++c) r ^= v[c];
-    out[blockIdx.x * blockDim.x + threadIdx.x] = r;
-}
+#define OPMAD24(x) asm volatile("v_mad_u32_u24 %0, %0, %1, %1" : "+v"(x) : "v"(s))
+#define OPPKADD16(x) asm volatile("v_pk_add_u16 %0, %0, %1" : "+v"(x) : "v"(s))
+KERNEL_U32(k_add, OPADD)
+KERNEL_U32(k_bcnt, OPBCNT)
+KERNEL_U32(k_cndmask, OPCND)
+KERNEL_U32(k_mul24sdwa, OPMUL)
+KERNEL_U32(k_mad24, OPMAD24)
+KERNEL_U32(k_pk_add_u16, OPPKADD16)
+
 __global__ __launch_bounds__(256) void k_fma(float *out, float s) {
     float v[8];
     for (int c = 0; c < 8; ++c) v[c] = threadIdx.x + c;
@@ -60,10 +51,42 @@ __global__ __launch_bounds__(256) void k_fma(float *out, float s) {
     for (int c = 0; c < 8; ++c) r += v[c];
     out[blockIdx.x * blockDim.x + threadIdx.x] = r;
 }
+__global__ __launch_bounds__(256) void k_mul_f32(float *out, float s) {
+    float v[8];
+    for (int c = 0; c < 8; ++c) v[c] = threadIdx.x + c;
+#define OPMULF(x) asm volatile("v_mul_f32 %0, %0, %1" : "+v"(x) : "v"(s))
+    CHAINS(OPMULF)
+    float r = 0;
+    for (int c = 0; c < 8; ++c) r += v[c];
+    out[blockIdx.x * blockDim.x + threadIdx.x] = r;
+}
+// packed f32: one instruction = two f32 operations per lane (64-bit register pairs)
+__global__ __launch_bounds__(256) void k_pk_mul_f32(float *out, float s) {
+    typedef float f2 __attribute__((ext_vector_type(2)));
+    f2 v[8];
+    const f2 ss = {s, s};
+    for (int c = 0; c < 8; ++c) v[c] = f2{(float)threadIdx.x + c, (float)c};
+#define OPPKMUL(x) asm volatile("v_pk_mul_f32 %0, %0, %1" : "+v"(x) : "v"(ss))
+    CHAINS(OPPKMUL)
+    float r = 0;
+    for (int c = 0; c < 8; ++c) r += v[c].x + v[c].y;
+    out[blockIdx.x * blockDim.x + threadIdx.x] = r;
+}
+__global__ __launch_bounds__(256) void k_pk_fma_f32(float *out, float s) {
+    typedef float f2 __attribute__((ext_vector_type(2)));
+    f2 v[8];
+    const f2 ss = {s, s};
+    for (int c = 0; c < 8; ++c) v[c] = f2{(float)threadIdx.x + c, (float)c};
+#define OPPKFMA(x) asm volatile("v_pk_fma_f32 %0, %0, %1, %1" : "+v"(x) : "v"(ss))
+    CHAINS(OPPKFMA)
+    float r = 0;
+    for (int c = 0; c < 8; ++c) r += v[c].x + v[c].y;
+    out[blockIdx.x * blockDim.x + threadIdx.x] = r;
+}
 
 template <typename K, typename T>
-void run(const char *name, K kern, T *d, T arg) {
-    const int blocks = 2048, threads = 256;
+void run(const char *name, K kern, T *d, T arg, int waves_per_simd, int ops_per_inst) {
+    const int threads = 256, blocks = 256 * waves_per_simd;  // 256 CUs x 4 SIMDs
     hipEvent_t a, b;
     hipEventCreate(&a);
     hipEventCreate(&b);
@@ -80,11 +103,11 @@ void run(const char *name, K kern, T *d, T arg) {
     const double insts = waves * kIters * 8;          // wave-instructions
     const double simds = 256.0 * 4;
     const double sec = ms * 1e-3;
-    // cycles per wave-instruction per SIMD at the reported peak clock (and the clock it implies at 2 / 4)
     const double cyc = sec * clk_khz * 1e3 * simds / insts;
-    printf("{\"op\": \"%s\", \"ms\": %.4f, \"cycles_per_wave_inst_per_simd_at_peak_clock\": %.3f, "
-           "\"peak_clock_MHz\": %.0f, \"wave_inst_per_s_per_simd\": %.4g, \"wave_inst_per_s_chip\": %.4g}\n",
-           name, ms, cyc, clk_khz / 1e3, insts / sec / simds, insts / sec);
+    printf("{\"op\": \"%s\", \"waves_per_simd\": %d, \"ops_per_lane_per_inst\": %d, \"ms\": %.4f, "
+           "\"cycles_per_wave_inst_per_simd_at_peak_clock\": %.3f, \"peak_clock_MHz\": %.0f, "
+           "\"wave_inst_per_s_per_simd\": %.4g, \"wave_inst_per_s_chip\": %.4g}\n",
+           name, waves_per_simd, ops_per_inst, ms, cyc, clk_khz / 1e3, insts / sec / simds, insts / sec);
 }
 
 int main() {
@@ -92,11 +115,18 @@ int main() {
     float *f;
     hipMalloc(&d, 2048 * 256 * 4);
     hipMalloc(&f, 2048 * 256 * 4);
-    run("v_add_u32", k_add, d, 3u);
-    run("v_bcnt", k_bcnt, d, 3u);
-    run("v_cndmask", k_cndmask, d, 3u);
-    run("v_mul24_sdwa", k_mul24sdwa, d, 3u);
-    run("v_fma_f32", k_fma, f, 1.0001f);
+    for (int w : {1, 2, 4, 8}) {
+        run("v_add_u32", k_add, d, 3u, w, 1);
+        run("v_bcnt", k_bcnt, d, 3u, w, 1);
+        run("v_cndmask", k_cndmask, d, 3u, w, 1);
+        run("v_mul24_sdwa", k_mul24sdwa, d, 3u, w, 1);
+        run("v_mad_u32_u24", k_mad24, d, 3u, w, 1);
+        run("v_pk_add_u16", k_pk_add_u16, d, 3u, w, 2);
+        run("v_fma_f32", k_fma, f, 1.0001f, w, 1);
+        run("v_mul_f32", k_mul_f32, f, 1.0001f, w, 1);
+        run("v_pk_mul_f32", k_pk_mul_f32, f, 1.0001f, w, 2);
+        run("v_pk_fma_f32", k_pk_fma_f32, f, 1.0001f, w, 2);
+    }
     hipFree(d);
     hipFree(f);
     return 0;
