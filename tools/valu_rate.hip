@@ -35,6 +35,48 @@ constexpr int kIters = 4096;  // x 8 chains x 8 unrolled ops
 #define OPMUL(x) asm volatile("v_mul_i32_i24_sdwa %0, sext(%0), %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_1 src1_sel:WORD_0" : "+v"(x) : "v"(s))
 #define OPMAD24(x) asm volatile("v_mad_u32_u24 %0, %0, %1, %1" : "+v"(x) : "v"(s))
 #define OPPKADD16(x) asm volatile("v_pk_add_u16 %0, %0, %1" : "+v"(x) : "v"(s))
+// encodings: _e32 = the 32-bit VOP1 / VOP2 form (VGPR second source; cndmask reads VCC), _e64 = the
+// 64-bit VOP3 form of the same operation
+#define OPADD32(x) asm volatile("v_add_u32_e32 %0, %0, %1" : "+v"(x) : "v"(s))
+#define OPADD64(x) asm volatile("v_add_u32_e64 %0, %0, %1" : "+v"(x) : "v"(s))
+#define OPAND32(x) asm volatile("v_and_b32_e32 %0, %0, %1" : "+v"(x) : "v"(s))
+#define OPAND64(x) asm volatile("v_and_b32_e64 %0, %0, %1" : "+v"(x) : "v"(s))
+#define OPXOR32(x) asm volatile("v_xor_b32_e32 %0, %0, %1" : "+v"(x) : "v"(s))
+#define OPLSH32(x) asm volatile("v_lshlrev_b32_e32 %0, 1, %0" : "+v"(x))
+#define OPCND32(x) asm volatile("v_cndmask_b32_e32 %0, %0, %1, vcc" : "+v"(x) : "v"(s))
+#define OPMOV32(x) asm volatile("v_mov_b32_e32 %0, %1" : "+v"(x) : "v"(s))
+#define OPNOT32(x) asm volatile("v_not_b32_e32 %0, %0" : "+v"(x))
+#define OPBFE(x) asm volatile("v_bfe_u32 %0, %0, 3, 9" : "+v"(x))
+#define OPADD3(x) asm volatile("v_add3_u32 %0, %0, %1, %1" : "+v"(x) : "v"(s))
+#define OPBITOP3(x) asm volatile("v_bitop3_b32 %0, %0, %1, %1 bitop3:0x1e" : "+v"(x) : "v"(s))
+#define OPDPP(x) asm volatile("v_add_u32_dpp %0, %0, %1 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf" : "+v"(x) : "v"(s))
+#define OPMUL24E32(x) asm volatile("v_mul_u32_u24_e32 %0, %0, %1" : "+v"(x) : "v"(s))
+#define OPANDC(x) asm volatile("v_and_b32_e32 %0, 0x7fffffff, %0" : "+v"(x))
+#define OPANDI(x) asm volatile("v_and_b32_e32 %0, 63, %0" : "+v"(x))
+#define OPANDS(x) asm volatile("v_and_b32_e32 %0, %1, %0" : "+v"(x) : "s"(s))
+#define OPLSHV(x) asm volatile("v_lshlrev_b32_e32 %0, %1, %0" : "+v"(x) : "v"(s))
+#define OPADDI(x) asm volatile("v_add_u32_e32 %0, 5, %0" : "+v"(x))
+#define OPBCNTV(x) asm volatile("v_bcnt_u32_b32 %0, %0, %1" : "+v"(x) : "v"(s))
+KERNEL_U32(k_andc, OPANDC)
+KERNEL_U32(k_andi, OPANDI)
+KERNEL_U32(k_ands, OPANDS)
+KERNEL_U32(k_lshv, OPLSHV)
+KERNEL_U32(k_addi, OPADDI)
+KERNEL_U32(k_bcntv, OPBCNTV)
+KERNEL_U32(k_add32, OPADD32)
+KERNEL_U32(k_add64, OPADD64)
+KERNEL_U32(k_and32, OPAND32)
+KERNEL_U32(k_and64, OPAND64)
+KERNEL_U32(k_xor32, OPXOR32)
+KERNEL_U32(k_lsh32, OPLSH32)
+KERNEL_U32(k_cnd32, OPCND32)
+KERNEL_U32(k_mov32, OPMOV32)
+KERNEL_U32(k_not32, OPNOT32)
+KERNEL_U32(k_bfe, OPBFE)
+KERNEL_U32(k_add3, OPADD3)
+KERNEL_U32(k_bitop3, OPBITOP3)
+KERNEL_U32(k_dpp, OPDPP)
+KERNEL_U32(k_mul24e32, OPMUL24E32)
 KERNEL_U32(k_add, OPADD)
 KERNEL_U32(k_bcnt, OPBCNT)
 KERNEL_U32(k_cndmask, OPCND)
@@ -110,11 +152,42 @@ void run(const char *name, K kern, T *d, T arg, int waves_per_simd, int ops_per_
            name, waves_per_simd, ops_per_inst, ms, cyc, clk_khz / 1e3, insts / sec / simds, insts / sec);
 }
 
-int main() {
+int main(int argc, char **argv) {
+    (void)argv;
     uint32_t *d;
     float *f;
     hipMalloc(&d, 2048 * 256 * 4);
     hipMalloc(&f, 2048 * 256 * 4);
+    const bool encodings = argc > 1;  // `valu_rate enc`: the encoding comparison only (4 and 8 waves)
+    if (encodings) {
+        for (int w : {4, 8}) {
+            run("v_and_b32 literal", k_andc, d, 3u, w, 1);
+            run("v_and_b32 inline const", k_andi, d, 3u, w, 1);
+            run("v_and_b32 sgpr", k_ands, d, 3u, w, 1);
+            run("v_lshlrev_b32 vgpr amount", k_lshv, d, 3u, w, 1);
+            run("v_add_u32 inline const", k_addi, d, 3u, w, 1);
+            run("v_bcnt_u32_b32 vgpr", k_bcntv, d, 3u, w, 1);
+            run("v_add_u32_e32", k_add32, d, 3u, w, 1);
+            run("v_add_u32_e64", k_add64, d, 3u, w, 1);
+            run("v_and_b32_e32", k_and32, d, 3u, w, 1);
+            run("v_and_b32_e64", k_and64, d, 3u, w, 1);
+            run("v_xor_b32_e32", k_xor32, d, 3u, w, 1);
+            run("v_lshlrev_b32_e32", k_lsh32, d, 3u, w, 1);
+            run("v_cndmask_b32_e32", k_cnd32, d, 3u, w, 1);
+            run("v_mov_b32_e32", k_mov32, d, 3u, w, 1);
+            run("v_not_b32_e32", k_not32, d, 3u, w, 1);
+            run("v_mul_u32_u24_e32", k_mul24e32, d, 3u, w, 1);
+            run("v_bfe_u32", k_bfe, d, 3u, w, 1);
+            run("v_add3_u32", k_add3, d, 3u, w, 1);
+            run("v_bitop3_b32", k_bitop3, d, 3u, w, 1);
+            run("v_add_u32_dpp", k_dpp, d, 3u, w, 1);
+            run("v_mul_f32", k_mul_f32, f, 1.0001f, w, 1);
+            run("v_fma_f32", k_fma, f, 1.0001f, w, 1);
+        }
+        hipFree(d);
+        hipFree(f);
+        return 0;
+    }
     for (int w : {1, 2, 4, 8}) {
         run("v_add_u32", k_add, d, 3u, w, 1);
         run("v_bcnt", k_bcnt, d, 3u, w, 1);
