@@ -234,7 +234,12 @@ __device__ __forceinline__ bool group_any(bool pred, int gbase) {
 enum : int { kContinue = -1, kAccept = 0, kFail = 1, kReject = 2, kNoCandidate = 3 };
 
 __device__ __forceinline__ void raise_status(uint32_t *status, uint32_t code, uint64_t panel) {
-    if (atomicCAS(&status[0], 0u, code) == 0u) {
+    // Materialise the operands here, on the rare path: left to itself the compiler keeps the constant
+    // code (and the zero compare value) in a VGPR pair across the whole draw loop, which spilled it in
+    // the register-bound kernels.
+    uint32_t c = code, z = 0u;
+    asm volatile("" : "+v"(c), "+v"(z));
+    if (atomicCAS(&status[0], z, c) == 0u) {
         status[1] = (uint32_t)panel;
         status[2] = (uint32_t)(panel >> 32);
     }
@@ -1124,6 +1129,10 @@ __global__ __launch_bounds__(kP2Threads, 1) void pair_fp4_tile_kernel(const uint
                     expand(rna, rnb, fna, fnb);
                     mfma(fca, fcb);
                 };
+                // (the spill slots of this kernel -- 58 VGPRs at MODE 2 -- are written and read in the
+                // prologue, the odd-block tail and the epilogue, once per item; the block loop has none.
+                // A wave-uniform skip of the last pair's second step inside the loop instead of this
+                // tail put 102 spill slots into the loop.)
                 int j = 0;
                 for (; j + 2 <= nb; j += 2) {
                     step(j, f0a, f0b, r1a, r1b, f1a, f1b, r0a, r0b);
@@ -2085,6 +2094,13 @@ int launch_draw(const csa_instance *I, int32_t k, uint64_t seed, uint64_t panel_
                        : cfg.wide ? wide_lds_bytes(cfg.G, cfg.FPL, cfg.WPL)
                                   : draw_lds_bytes(cfg.G, cfg.FPL, cfg.WPL, I->W, k, groups_wg);
     if (lds > 160 * 1024) return fail(CSA_E_UNSUPPORTED, "draw kernel needs %zu B of LDS", lds);
+    // CSA_DRAW_LDS_PAD (diagnostic A/B only): extra bytes of LDS per register-kernel workgroup, to price
+    // the occupancy an LDS-resident pick-list tile would cost (128 panels x kpad u16 = 28 KB at sf_e)
+    static const size_t lds_pad = [] {
+        const char *e = getenv("CSA_DRAW_LDS_PAD");
+        return e ? (size_t)strtoull(e, nullptr, 10) : (size_t)0;
+    }();
+    const size_t lds_launch = (cfg.lane || cfg.solo) && lds + lds_pad <= 160 * 1024 ? lds + lds_pad : lds;
     const uint64_t want = (n_panels + groups_wg - 1) / groups_wg;
     // the lane kernel: one workgroup per 128 panels, not persistent -- sf_e 10^6 panels: 4.47 ms vs
     // 5.05 ms for a persistent grid, and retiring workgroups let a concurrent stream's kernels in.
@@ -2104,7 +2120,7 @@ int launch_draw(const csa_instance *I, int32_t k, uint64_t seed, uint64_t panel_
         A.hashes = nullptr;
     }
     void *args[] = {&A};
-    HIPCHK(hipLaunchKernel(cfg.fn, dim3((unsigned)std::max<uint64_t>(1, grid)), dim3(threads), args, lds, stream));
+    HIPCHK(hipLaunchKernel(cfg.fn, dim3((unsigned)std::max<uint64_t>(1, grid)), dim3(threads), args, lds_launch, stream));
     HIPCHK(hipGetLastError());
     if (!single && !d_panel_list) M->panels_drawn += n_panels;  // (index-list re-draws are not new panels)
     if (cfg.picks() && !d_picks_ext) {  // pick lists -> packed panels (+ hashes)

@@ -57,6 +57,46 @@ constexpr int kIters = 4096;  // x 8 chains x 8 unrolled ops
 #define OPLSHV(x) asm volatile("v_lshlrev_b32_e32 %0, %1, %0" : "+v"(x) : "v"(s))
 #define OPADDI(x) asm volatile("v_add_u32_e32 %0, 5, %0" : "+v"(x))
 #define OPBCNTV(x) asm volatile("v_bcnt_u32_b32 %0, %0, %1" : "+v"(x) : "v"(s))
+#define OP_k_or32(x) asm volatile("v_or_b32_e32 %0, %0, %1" : "+v"(x) : "v"(s))
+KERNEL_U32(k_or32, OP_k_or32)
+#define OP_k_sub32(x) asm volatile("v_sub_u32_e32 %0, %0, %1" : "+v"(x) : "v"(s))
+KERNEL_U32(k_sub32, OP_k_sub32)
+#define OP_k_max32(x) asm volatile("v_max_u32_e32 %0, %0, %1" : "+v"(x) : "v"(s))
+KERNEL_U32(k_max32, OP_k_max32)
+#define OP_k_min32(x) asm volatile("v_min_u32_e32 %0, %0, %1" : "+v"(x) : "v"(s))
+KERNEL_U32(k_min32, OP_k_min32)
+#define OP_k_lshr32(x) asm volatile("v_lshrrev_b32_e32 %0, %1, %0" : "+v"(x) : "v"(s))
+KERNEL_U32(k_lshr32, OP_k_lshr32)
+#define OP_k_lshlor(x) asm volatile("v_lshl_or_b32 %0, %0, 3, %1" : "+v"(x) : "v"(s))
+KERNEL_U32(k_lshlor, OP_k_lshlor)
+#define OP_k_andor(x) asm volatile("v_and_or_b32 %0, %0, %1, %1" : "+v"(x) : "v"(s))
+KERNEL_U32(k_andor, OP_k_andor)
+#define OP_k_bfi(x) asm volatile("v_bfi_b32 %0, %0, %1, %1" : "+v"(x) : "v"(s))
+KERNEL_U32(k_bfi, OP_k_bfi)
+#define OP_k_alignbit(x) asm volatile("v_alignbit_b32 %0, %0, %1, 7" : "+v"(x) : "v"(s))
+KERNEL_U32(k_alignbit, OP_k_alignbit)
+#define OP_k_perm(x) asm volatile("v_perm_b32 %0, %0, %1, %1" : "+v"(x) : "v"(s))
+KERNEL_U32(k_perm, OP_k_perm)
+#define OP_k_mulhi(x) asm volatile("v_mul_hi_u32 %0, %0, %1" : "+v"(x) : "v"(s))
+KERNEL_U32(k_mulhi, OP_k_mulhi)
+#define OP_k_mullo(x) asm volatile("v_mul_lo_u32 %0, %0, %1" : "+v"(x) : "v"(s))
+KERNEL_U32(k_mullo, OP_k_mullo)
+#define OP_k_cmpvcc(x) asm volatile("v_cmp_gt_u32_e32 vcc, %0, %1\n v_mov_b32_e32 %0, %0" : "+v"(x) : "v"(s) : "vcc")
+KERNEL_U32(k_cmpvcc, OP_k_cmpvcc)
+#define OP_k_movdpp(x) asm volatile("v_mov_b32_dpp %0, %1 row_shr:1 row_mask:0xf bank_mask:0xf" : "+v"(x) : "v"(s))
+KERNEL_U32(k_movdpp, OP_k_movdpp)
+#define OP_k_cndvcc(x) asm volatile("v_cmp_gt_u32_e32 vcc, %1, %0\n v_cndmask_b32_e32 %0, %0, %1, vcc" : "+v"(x) : "v"(s) : "vcc")
+KERNEL_U32(k_cndvcc, OP_k_cndvcc)
+#define OP_k_cndsg(x) asm volatile("v_cndmask_b32_e64 %0, %0, %1, s[40:41]" : "+v"(x) : "v"(s) : "s40", "s41")
+KERNEL_U32(k_cndsg, OP_k_cndsg)
+#define OP_k_cmpsg(x) asm volatile("v_cmp_gt_u32_e64 s[40:41], %0, %1\n v_mov_b32_e32 %0, %0" : "+v"(x) : "v"(s) : "s40", "s41")
+KERNEL_U32(k_cmpsg, OP_k_cmpsg)
+#define OP_k_sadu(x) asm volatile("v_max3_u32 %0, %0, %1, %1" : "+v"(x) : "v"(s))
+KERNEL_U32(k_sadu, OP_k_sadu)
+#define OP_k_pkadd16v(x) asm volatile("v_pk_add_u16 %0, %0, %1" : "+v"(x) : "v"(s))
+KERNEL_U32(k_pkadd16v, OP_k_pkadd16v)
+#define OP_k_addco(x) asm volatile("v_add_co_u32_e32 %0, vcc, %0, %1" : "+v"(x) : "v"(s) : "vcc")
+KERNEL_U32(k_addco, OP_k_addco)
 KERNEL_U32(k_andc, OPANDC)
 KERNEL_U32(k_andi, OPANDI)
 KERNEL_U32(k_ands, OPANDS)
@@ -64,6 +104,28 @@ KERNEL_U32(k_lshv, OPLSHV)
 KERNEL_U32(k_addi, OPADDI)
 KERNEL_U32(k_bcntv, OPBCNTV)
 KERNEL_U32(k_add32, OPADD32)
+
+// Mixed streams: chain c runs FULL when c % PERIOD < NFULL, else HALF; the cycles per instruction against
+// the weighted mean of the pure rates say whether the two classes add up or overlap.
+#define MIXK(NAME, FULLOP, HALFOP, PERIOD, NFULL)                                       \
+    __global__ __launch_bounds__(256) void NAME(uint32_t *out, uint32_t s) {            \
+        uint32_t v[8];                                                                  \
+        for (int c = 0; c < 8; ++c) v[c] = threadIdx.x + c;                             \
+        for (int i = 0; i < kIters; ++i) {                                              \
+            _Pragma("unroll") for (int c = 0; c < 8; ++c) {                             \
+                if (c % PERIOD < NFULL) { FULLOP(v[c]); } else { HALFOP(v[c]); }        \
+            }                                                                           \
+        }                                                                               \
+        uint32_t r = 0;                                                                 \
+        for (int c = 0; c < 8; ++c) r ^= v[c];                                          \
+        out[blockIdx.x * blockDim.x + threadIdx.x] = r;                                 \
+    }
+MIXK(k_mix_add_bcnt_11, OPADD32, OPBCNTV, 2, 1)
+MIXK(k_mix_add_bcnt_31, OPADD32, OPBCNTV, 4, 3)
+MIXK(k_mix_add_bcnt_13, OPADD32, OPBCNTV, 4, 1)
+MIXK(k_mix_and_lshl_11, OPAND32, OPLSHV, 2, 1)
+MIXK(k_mix_add_mulhi_11, OPADD32, OP_k_mulhi, 2, 1)
+MIXK(k_mix_xor_bitop3_11, OPXOR32, OPBITOP3, 2, 1)
 KERNEL_U32(k_add64, OPADD64)
 KERNEL_U32(k_and32, OPAND32)
 KERNEL_U32(k_and64, OPAND64)
@@ -161,6 +223,32 @@ int main(int argc, char **argv) {
     const bool encodings = argc > 1;  // `valu_rate enc`: the encoding comparison only (4 and 8 waves)
     if (encodings) {
         for (int w : {4, 8}) {
+            run("mix add:bcnt 1:1", k_mix_add_bcnt_11, d, 3u, w, 1);
+            run("mix add:bcnt 3:1", k_mix_add_bcnt_31, d, 3u, w, 1);
+            run("mix add:bcnt 1:3", k_mix_add_bcnt_13, d, 3u, w, 1);
+            run("mix and:lshlrev 1:1", k_mix_and_lshl_11, d, 3u, w, 1);
+            run("mix add:mul_hi 1:1", k_mix_add_mulhi_11, d, 3u, w, 1);
+            run("mix xor:bitop3 1:1", k_mix_xor_bitop3_11, d, 3u, w, 1);
+            run("v_or_b32_e32", k_or32, d, 3u, w, 1);
+            run("v_sub_u32_e32", k_sub32, d, 3u, w, 1);
+            run("v_max_u32_e32", k_max32, d, 3u, w, 1);
+            run("v_min_u32_e32", k_min32, d, 3u, w, 1);
+            run("v_lshrrev_b32_e32 vgpr", k_lshr32, d, 3u, w, 1);
+            run("v_lshl_or_b32", k_lshlor, d, 3u, w, 1);
+            run("v_and_or_b32", k_andor, d, 3u, w, 1);
+            run("v_bfi_b32", k_bfi, d, 3u, w, 1);
+            run("v_alignbit_b32", k_alignbit, d, 3u, w, 1);
+            run("v_perm_b32", k_perm, d, 3u, w, 1);
+            run("v_mul_hi_u32", k_mulhi, d, 3u, w, 1);
+            run("v_mul_lo_u32", k_mullo, d, 3u, w, 1);
+            run("v_cmp_gt_u32_e32 (vcc)", k_cmpvcc, d, 3u, w, 1);
+            run("v_mov_b32_dpp row_shr:1", k_movdpp, d, 3u, w, 1);
+            run("v_cndmask_b32_e32 after vcc write", k_cndvcc, d, 3u, w, 1);
+            run("v_cndmask_b32_e64 sgpr cond", k_cndsg, d, 3u, w, 1);
+            run("v_cmp_gt_u32_e64 -> sgpr", k_cmpsg, d, 3u, w, 1);
+            run("v_max3_u32", k_sadu, d, 3u, w, 1);
+            run("v_pk_add_u16 vgpr", k_pkadd16v, d, 3u, w, 1);
+            run("v_add_co_u32_e32", k_addco, d, 3u, w, 1);
             run("v_and_b32 literal", k_andc, d, 3u, w, 1);
             run("v_and_b32 inline const", k_andi, d, 3u, w, 1);
             run("v_and_b32 sgpr", k_ands, d, 3u, w, 1);
