@@ -607,28 +607,79 @@ __global__ __launch_bounds__(256) void panel_hash_kernel(const uint64_t *__restr
 constexpr int kXtThreads = 256;
 constexpr int kXtBlocksPerGroup = 16;  // at most 1024 panels per workgroup
 
-// 64x64 bit-matrix transpose across a wavefront: lane i holds row i (bit j = column j);
-// afterwards lane j holds column j (bit i = row i).
-__device__ __forceinline__ uint64_t wave_transpose64(uint64_t x, int lane) {
-    const uint64_t masks[6] = {0x00000000FFFFFFFFull, 0x0000FFFF0000FFFFull, 0x00FF00FF00FF00FFull,
-                               0x0F0F0F0F0F0F0F0Full, 0x3333333333333333ull, 0x5555555555555555ull};
-#pragma unroll
-    for (int t = 0; t < 6; ++t) {
-        const int s = 32 >> t;
-        const uint64_t M = masks[t];
-        const uint64_t y = (uint64_t)__shfl_xor((long long)x, s);
-        if (lane & s)
-            x = (x & ~M) | ((y & ~M) >> s);
-        else
-            x = (x & M) | ((y & M) << s);
+// 64x64 bit-matrix transpose across a wavefront, in registers: lane i holds row i (bit j = column
+// j) as (lo, hi) 32-bit halves; afterwards lane j holds column j (bit i = row i).  The six butterfly
+// stages (stage s trades the bit-s half of the column index with lane bit s) run on VALU
+// cross-lane moves only -- no ds_bpermute, no divergent branches (the round-2 form: 12 bpermutes and
+// both sides of a lane-bit branch per stage):
+//   s = 32: one v_permlane32_swap (lanes 32-63 of lo <-> lanes 0-31 of hi);
+//   s = 16: the 16-bit fields each lane keeps / gives are gathered into two registers (v_perm), one
+//           v_permlane16_swap trades the given ones between rows 2r and 2r+1, two v_perm re-interleave;
+//   s = 8:  the given bytes gathered by a lane-dependent v_perm, DPP row_ror:8 (= lane ^ 8), two
+//           lane-dependent v_perm merge;
+//   s = 4, 2, 1: the partner's word by DPP (quad_perm xor 3 + row_half_mirror = lane ^ 4; quad_perm
+//           for ^ 2, ^ 1), rotated into place by v_alignbit, merged by v_bfi with the lane's keep mask.
+// 30 VALU per 64x64 block; the stage algebra is modelled lane by lane and checked in
+// tests/test_host_logic.py::test_xt_register_transpose_network.
+struct XtLane {
+    uint32_t s8_send, s8_lo, s8_hi;  // stage 8 byte selectors
+    uint32_t k4, k2, k1;             // keep masks of stages 4, 2, 1
+    uint32_t r4, r2, r1;             // rotate amounts of stages 4, 2, 1
+};
+__device__ __forceinline__ XtLane xt_lane_consts(int lane) {
+    XtLane c;
+    const bool b3 = (lane >> 3) & 1, b2 = (lane >> 2) & 1, b1 = (lane >> 1) & 1, b0 = lane & 1;
+    c.s8_send = b3 ? 0x06040200u : 0x07050301u;
+    c.s8_lo = b3 ? 0x03050104u : 0x05020400u;
+    c.s8_hi = b3 ? 0x03070106u : 0x07020600u;
+    c.k4 = b2 ? 0xF0F0F0F0u : 0x0F0F0F0Fu;
+    c.k2 = b1 ? 0xCCCCCCCCu : 0x33333333u;
+    c.k1 = b0 ? 0xAAAAAAAAu : 0x55555555u;
+    c.r4 = b2 ? 4u : 28u;
+    c.r2 = b1 ? 2u : 30u;
+    c.r1 = b0 ? 1u : 31u;
+    return c;
+}
+template <int CTRL>
+__device__ __forceinline__ uint32_t xt_dpp(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xF, 0xF, true);
+}
+__device__ __forceinline__ uint32_t xt_merge(uint32_t x, uint32_t y, uint32_t keep, uint32_t rot) {
+    const uint32_t t = __builtin_amdgcn_alignbit(y, y, rot);  // y rotated right by rot
+    return (keep & x) | (~keep & t);                        // v_bfi
+}
+__device__ __forceinline__ void wave_transpose64(uint32_t &lo, uint32_t &hi, const XtLane &c) {
+    {  // s = 32
+        const auto r = __builtin_amdgcn_permlane32_swap(lo, hi, false, false);
+        lo = r[0];
+        hi = r[1];
     }
-    return x;
+    {  // s = 16
+        const uint32_t A = __builtin_amdgcn_perm(hi, lo, 0x05040100u), B = __builtin_amdgcn_perm(hi, lo, 0x07060302u);
+        const auto r = __builtin_amdgcn_permlane16_swap(A, B, false, false);
+        lo = __builtin_amdgcn_perm(r[1], r[0], 0x05040100u);
+        hi = __builtin_amdgcn_perm(r[1], r[0], 0x07060302u);
+    }
+    {  // s = 8
+        const uint32_t R = xt_dpp<0x128>(__builtin_amdgcn_perm(hi, lo, c.s8_send));  // row_ror:8
+        lo = __builtin_amdgcn_perm(R, lo, c.s8_lo);
+        hi = __builtin_amdgcn_perm(R, hi, c.s8_hi);
+    }
+    // s = 4: quad_perm [3,2,1,0] then row_half_mirror = lane ^ 4
+    lo = xt_merge(lo, xt_dpp<0x141>(xt_dpp<0x1B>(lo)), c.k4, c.r4);
+    hi = xt_merge(hi, xt_dpp<0x141>(xt_dpp<0x1B>(hi)), c.k4, c.r4);
+    lo = xt_merge(lo, xt_dpp<0x4E>(lo), c.k2, c.r2);  // s = 2: quad_perm [2,3,0,1]
+    hi = xt_merge(hi, xt_dpp<0x4E>(hi), c.k2, c.r2);
+    lo = xt_merge(lo, xt_dpp<0xB1>(lo), c.k1, c.r1);  // s = 1: quad_perm [1,0,3,2]
+    hi = xt_merge(hi, xt_dpp<0xB1>(hi), c.k1, c.r1);
 }
 
 // blockIdx.y = column range: words [CW y, CW y + CW) of every panel, i.e. agents [64 CW y, ...).
 // 32 words per range: a 17 KB tile + 8 KB of counts per workgroup, so ~6 workgroups share a CU and
 // one's loads overlap another's transposes (128-word ranges at n = 8192 needed 98 KB, one
-// workgroup per CU, and moved 2 GB per 10^6 panels at 0.9 TB/s)
+// workgroup per CU, and moved 2 GB per 10^6 panels at 0.9 TB/s).  Inside a workgroup the next
+// block's panel words are loaded into registers while the current block is transposed (thread t
+// loads rows t/32 + 8q, word t%32: no integer division per element).
 constexpr int kXtCols = 32;
 __global__ __launch_bounds__(kXtThreads) void xt_count_kernel(const uint64_t *__restrict__ panels,
                                                               uint64_t S, int n, int W, int npad,
@@ -641,31 +692,47 @@ __global__ __launch_bounds__(kXtThreads) void xt_count_kernel(const uint64_t *__
     uint64_t *tile = smem;                                   // 64 x Wp
     uint32_t *cnt = reinterpret_cast<uint32_t *>(smem + 64 * Wp);  // np
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nwv = blockDim.x >> 6;
+    const XtLane tc = xt_lane_consts(lane);
     for (int p = threadIdx.x; p < np; p += blockDim.x) cnt[p] = 0;
     const uint64_t nblk = (S + 63) / 64;
     const uint64_t b0 = (uint64_t)blockIdx.x * bpg;
     const uint64_t b1 = min(nblk, b0 + (uint64_t)bpg);
     const int ncol = min(npad / 64 - c0, kXtCols);  // transposed columns (padding included)
-    for (uint64_t b = b0; b < b1; ++b) {
-        __syncthreads();
+    static_assert(kXtThreads == 256 && kXtCols == 32, "loader: 8 rows of 32 words per pass");
+    const int lr = threadIdx.x >> 5, lc = threadIdx.x & 31;
+    uint64_t pre[8];
+    auto load_blk = [&](uint64_t b) {
         const uint64_t row0 = b * 64;
         const int rows = (int)min<uint64_t>(64, S - row0);
-        const uint64_t *src = panels + row0 * (uint64_t)W + c0;
-        for (int t = threadIdx.x; t < 64 * CW; t += blockDim.x) {
-            const int r = t / CW, c = t - r * CW;
-            tile[r * Wp + c] = r < rows ? src[(uint64_t)r * W + c] : 0ull;
+        // branch-free: out-of-range rows / words load a clamped in-range address and are zeroed
+        const uint64_t *src = panels + row0 * (uint64_t)W + c0 + min(lc, CW - 1);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const int r = lr + 8 * q;
+            const uint64_t v = src[(uint64_t)min(r, rows - 1) * W];
+            pre[q] = (lc < CW && r < rows) ? v : 0ull;
+        }
+    };
+    if (b0 < b1) load_blk(b0);
+    for (uint64_t b = b0; b < b1; ++b) {
+        __syncthreads();  // every wave is done with the previous block's tile
+        if (lc < CW) {
+#pragma unroll
+            for (int q = 0; q < 8; ++q) tile[(lr + 8 * q) * Wp + lc] = pre[q];
         }
         __syncthreads();
+        if (b + 1 < b1) load_blk(b + 1);  // in flight while this block is transposed
         for (int w = wv; w < ncol; w += nwv) {
-            uint64_t x = w < CW ? tile[lane * Wp + w] : 0ull;
-            x = wave_transpose64(x, lane);
+            const uint64_t x = w < CW ? tile[lane * Wp + w] : 0ull;
+            uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+            wave_transpose64(lo, hi, tc);
             const int p = 64 * w + lane;
             if (xt) {  // two 32-bit planes per panel block: panels 64b..64b+31, then 64b+32..64b+63
                 uint32_t *x32 = reinterpret_cast<uint32_t *>(xt) + 2 * b * (uint64_t)npad + p0 + p;
-                x32[0] = (uint32_t)x;
-                x32[npad] = (uint32_t)(x >> 32);
+                x32[0] = lo;
+                x32[npad] = hi;
             }
-            if (p < np) cnt[p] += (uint32_t)__popcll(x);
+            if (p < np) cnt[p] += (uint32_t)(__popc(lo) + __popc(hi));
         }
     }
     __syncthreads();

@@ -257,3 +257,74 @@ def test_result_tuple_pickles_host_only():
     assert len(empty) == 7
     with pytest.raises(RuntimeError):
         iter(empty)
+
+
+def _xt_network(X):
+    """Numpy model of xt_count_kernel's register transpose (csrc/csa_legacy.hip, wave_transpose64):
+    the same v_perm selectors, lane swaps, DPP patterns, rotations and keep masks, lane by lane."""
+    M = 0xFFFFFFFF
+    lane = np.arange(64)
+    lo = [int(x) & M for x in X]
+    hi = [int(x) >> 32 for x in X]
+
+    def perm(s0, s1, sel):
+        out = []
+        for i in range(64):
+            v = (s0[i] << 32) | s1[i]
+            sl = sel[i] if isinstance(sel, list) else sel
+            out.append(sum(((v >> (8 * ((sl >> (8 * k)) & 0xFF))) & 0xFF) << (8 * k) for k in range(4)))
+        return out
+
+    def rot(y, r):
+        return [((y[i] >> r[i]) | (y[i] << (32 - r[i]))) & M for i in range(64)]
+
+    def move(x, f):
+        return [x[f(i)] for i in range(64)]
+
+    # s = 32: permlane32_swap(lo, hi): lanes 32-63 of lo <-> lanes 0-31 of hi
+    lo, hi = lo[:32] + hi[:32], lo[32:] + hi[32:]
+    # s = 16: gather, permlane16_swap (odd rows of A <-> even rows of B), re-interleave
+    A, B = perm(hi, lo, 0x05040100), perm(hi, lo, 0x07060302)
+    A2, B2 = A[:], B[:]
+    for r in (0, 32):
+        A2[r + 16:r + 32], B2[r:r + 16] = B[r:r + 16], A[r + 16:r + 32]
+    lo, hi = perm(B2, A2, 0x05040100), perm(B2, A2, 0x07060302)
+    # s = 8: lane-dependent byte gather, row_ror:8, lane-dependent merges
+    b3 = [(i >> 3) & 1 for i in range(64)]
+    sel = lambda one, zero: [one if b else zero for b in b3]  # noqa: E731
+    R = move(perm(hi, lo, sel(0x06040200, 0x07050301)), lambda i: (i & ~15) | ((i + 8) & 15))
+    lo, hi = perm(R, lo, sel(0x03050104, 0x05020400)), perm(R, hi, sel(0x03070106, 0x07020600))
+    for s, keep0, f in ((4, 0x0F0F0F0F, lambda i: i ^ 4),
+                        (2, 0x33333333, lambda i: i ^ 2), (1, 0x55555555, lambda i: i ^ 1)):
+        bit = (lane // s) & 1
+        keep = [(~keep0 & M) if b else keep0 for b in bit]
+        r = [s if b else 32 - s for b in bit]
+        out = []
+        for h in (lo, hi):
+            t = rot(move(h, f), r)
+            out.append([(keep[i] & h[i]) | (~keep[i] & M & t[i]) for i in range(64)])
+        lo, hi = out
+    return [(hi[i] << 32) | lo[i] for i in range(64)]
+
+
+def test_xt_register_transpose_network():
+    import os
+    import re
+    rng = np.random.default_rng(7)
+    X = rng.integers(0, 2 ** 63, size=64, dtype=np.uint64) | (rng.integers(0, 2, 64, dtype=np.uint64) << np.uint64(63))
+    Y = _xt_network(X)
+    bits = np.array([[(int(X[i]) >> j) & 1 for j in range(64)] for i in range(64)])
+    tb = np.array([[(Y[j] >> i) & 1 for i in range(64)] for j in range(64)])
+    assert (bits.T == tb).all()
+    # DPP lane ^ 4 = quad_perm [3,2,1,0] (^3) then row_half_mirror (7 - i within 8 lanes)
+    assert all(((i & ~7) | (7 - ((i ^ 3) & 7))) == i ^ 4 for i in range(64))
+    # the model's constants are the kernel's
+    src = open(os.path.join(os.path.dirname(__file__), "..", "citizensassemblies-replication_amd", "csrc",
+                            "csa_legacy.hip")).read()
+    body = src[src.index("__device__ __forceinline__ XtLane xt_lane_consts"):src.index("constexpr int kXtCols")]
+    for c in ("0x05040100u", "0x07060302u", "0x06040200u", "0x07050301u", "0x03050104u", "0x05020400u",
+              "0x03070106u", "0x07020600u", "0xF0F0F0F0u", "0x0F0F0F0Fu", "0xCCCCCCCCu", "0x33333333u",
+              "0xAAAAAAAAu", "0x55555555u", "xt_dpp<0x128>", "xt_dpp<0x141>(xt_dpp<0x1B>", "xt_dpp<0x4E>",
+              "xt_dpp<0xB1>"):
+        assert c in body, c
+    assert re.search(r"c\.r4 = b2 \? 4u : 28u", body)
