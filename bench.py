@@ -196,8 +196,10 @@ def cpu_baseline(inst_dir, k, seed, target_s, want_pairs):
 def load_valu_peak():
     """Integer VALU issue roof of one MI355X (wave-instructions/s over the chip): tools/valu_rate.hip
     on the GPU box, 8 waves/SIMD of independent v_add_u32 / v_bcnt / v_cndmask / v_mul_i32_i24_sdwa
-    chains (profiles/valu_rate_mi355x.jsonl).  A wave64 integer VALU instruction occupies its SIMD
-    ~4.3 cycles at the 2.4 GHz peak clock, not the 2 of an f32 FMA's nominal rate."""
+    chains (profiles/valu_rate_mi355x.jsonl): the ~4.2-cycle class of wave64 instructions (an SGPR
+    operand, bcnt, cndmask, mul24, shifts left, 3-source ops, DPP).  Two-operand add/and/or/xor/mov with
+    VGPR or constant operands issue every ~2.3 cycles in a homogeneous stream but not in the draw
+    kernels' mixed ones (profiles/valu_enc_mi355x.jsonl), so this is the roof."""
     path = os.path.join(REPO, "profiles", "valu_rate_mi355x.jsonl")
     if not os.path.exists(path):
         return None
