@@ -111,6 +111,33 @@ def test_devices_legacy_probabilities(gpu_available):
     assert hist.upper().tolist() == (np.asarray(g["pair_upper"]) / g["S"]).tolist()
 
 
+def _hip_device_count():
+    N = pkg("_native")
+    out = np.zeros(1, np.int32)
+    return int(out[0]) if N.lib().csa_device_count(N.ptr(out)) == N.CSA_OK else 0
+
+
+@pytest.mark.parametrize("name,k,S,seed", [
+    ("couples_panel_from_twenty_people_no_constraints_2", 2, 10000, 0),   # duplicates across the devices
+    ("sf_e_110", 110, 200000, 4),                                          # partitioned distinct pass per shard
+    ("synthetic8192_200", 200, 5000, 2),                                   # n = 8192 pair sums over peer copies
+])
+def test_distinct_devices_equal_single_call(gpu_available, name, k, S, seed):
+    """Shards on DIFFERENT GPUs: the peer copies of counts, pairs and distinct segments into shard 0's
+    device, the replicas on the other devices, the cross-device stream ordering.  Runs only on a box
+    with >= 2 GPUs (the driver's 8-GPU node); one-GPU boxes cover the same code with device 0 repeated."""
+    ndev = _hip_device_count()
+    if ndev < 2:
+        pytest.skip("needs >= 2 HIP devices (this box has %d)" % ndev)
+    A = pkg("analysis")
+    _, enc = _enc(name, k)
+    one = A.legacy_sample_raw(enc, k, S, seed, want_pairs=True, want_panels=True, want_attempts=True)
+    for devs in ([0, 1], list(range(ndev)), [1, 0, 1]):
+        many = A.legacy_sample_raw(enc, k, S, seed, want_pairs=True, want_panels=True, want_attempts=True,
+                                   devices=devs)
+        _same(one, many, enc.n)
+
+
 def test_devices_bad_arguments(gpu_available):
     N = pkg("_native")
     L = N.lib()
