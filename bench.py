@@ -449,16 +449,19 @@ def main():
             j = args.warmup + args.steps - 1
             ndev = max(torch.cuda.device_count(), 1)
             devs = [(dev_index + s_) % ndev for s_ in range(world)]
-            raw = A.legacy_sample_raw(enc, k, S * world, args.seed, panel_begin=j * world * S, want_pairs=want_pairs,
-                                      want_panels=False, devices=devs)
-            got_c = pipe.counts.cpu().numpy()
-            same = bool((raw.counts == got_c).all()) and raw.unique == checks["last_step_unique"]
-            if want_pairs:
-                import numpy as np
-                got_p = pipe.pairs.view(enc.n, enc.n).cpu().numpy()
-                same = same and bool(np.array_equal(np.triu(raw.pairs), np.triu(got_p)))
-            checks["sample_devices"] = {"devices": devs, "panels": S * world, "unique": raw.unique,
-                                        "equal_to_rank_sharded": same}
+            try:
+                raw = A.legacy_sample_raw(enc, k, S * world, args.seed, panel_begin=j * world * S,
+                                          want_pairs=want_pairs, want_panels=False, devices=devs)
+                got_c = pipe.counts.cpu().numpy()
+                same = bool((raw.counts == got_c).all()) and raw.unique == checks["last_step_unique"]
+                if want_pairs:
+                    import numpy as np
+                    got_p = pipe.pairs.view(enc.n, enc.n).cpu().numpy()
+                    same = same and bool(np.array_equal(np.triu(raw.pairs), np.triu(got_p)))
+                checks["sample_devices"] = {"devices": devs, "panels": S * world, "unique": raw.unique,
+                                            "equal_to_rank_sharded": same}
+            except Exception as e:   # a check after the timed region: report it, never strand the other ranks
+                checks["sample_devices"] = {"devices": devs, "error": "%s: %s" % (type(e).__name__, e)}
         dist.barrier()
 
     def stage_times(rec):
