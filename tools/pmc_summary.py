@@ -20,7 +20,7 @@ from collections import defaultdict
 
 
 def short(name):
-    m = re.search(r"(draw_kernel<[^>]*>|pair_mfma_kernel|xt_count_kernel|unique_kernel|[A-Za-z_]+kernel[^(]*)", name)
+    m = re.search(r"(draw_kernel<[^>]*>|pair_mfma_kernel|xt_count_kernel|unique_kernel|[A-Za-z0-9_]+kernel[^(]*)", name)
     return m.group(1) if m else name[:60]
 
 
