@@ -240,3 +240,58 @@ def test_one_lane_layouts_match_oracle(gpu_available, F_per_cat, n, k):
     assert rc == 0
     assert np.array_equal(attempts, oatt)
     assert np.array_equal(panels, opanels)
+
+
+def _synthetic_tight(F_per_cat, n, k, seed, lo=0.9, hi=1.1):
+    """As _synthetic with quotas floor(lo k p) / ceil(hi k p): lo, hi near 1 make restarts frequent."""
+    rng = np.random.default_rng(seed)
+    cats, feats, fmin, fmax, fcat, shares = {}, [], [], [], [], []
+    for c, nf in enumerate(F_per_cat):
+        p = rng.dirichlet(np.full(nf, 2.0))
+        shares.append(p)
+        cats["c%d" % c] = {}
+        for j in range(nf):
+            a, b = int(np.floor(lo * k * p[j])), int(np.ceil(hi * k * p[j]))
+            cats["c%d" % c]["f%d" % j] = {"min": a, "max": b}
+            feats.append(("c%d" % c, "f%d" % j))
+            fmin.append(a)
+            fmax.append(b)
+            fcat.append(c)
+    picks = [rng.choice(len(p), size=n, p=p) for p in shares]
+    agents = {i: {"c%d" % c: "f%d" % picks[c][i] for c in range(len(F_per_cat))} for i in range(n)}
+    pf = [[feats.index(("c%d" % c, "f%d" % picks[c][i])) for c in range(len(F_per_cat))] for i in range(n)]
+    o = OracleInstance(k=k, cat_names=list(cats), feat_names=feats, fmin=fmin, fmax=fmax, fcat=fcat,
+                       person_feat=pf)
+    return cats, agents, o
+
+
+@pytest.mark.parametrize("F_per_cat,n,k,lo,hi,want", [
+    ((4, 4, 4, 4, 4), 3000, 120, 0.9, 1.1, "draw_wide_kernel<8, 4, 8>"),    # W = 47: 8 words per lane
+    ((8,) * 8, 3900, 150, 0.9, 1.1, "draw_wide_kernel<8, 8, 8>"),          # F = 64: 8 features per lane
+    ((6,) * 10, 8000, 200, 0.95, 1.05, "draw_wide_kernel<8, 8, 16>"),      # F = 60, W = 125, restarts
+    ((3, 4, 5), 2500, 90, 0.97, 1.03, "draw_wide_kernel<8, 2, 8>"),        # F = 12 past the lane kernel's W
+])
+def test_wide_layouts_match_oracle(gpu_available, F_per_cat, n, k, lo, hi, want):
+    """draw_wide_kernel's feature / word splits the public instances do not reach (FPL 2 / 4 / 8, WPL 8 /
+    16, ragged last lanes), on synthetic pools against the C oracle: panels, attempts and the restart
+    counters, through the default routing (n > 2048 or W > 32 takes the wide kernel)."""
+    import ctypes
+    P = pkg()
+    N = pkg("_native")
+    A = pkg("analysis")
+    cats, agents, o = _synthetic_tight(F_per_cat, n, k, seed=n + k, lo=lo, hi=hi)
+    enc = P.encode(cats, agents)
+    buf = np.zeros(64, np.uint8)
+    N.check(N.lib().csa_draw_kernel_name(enc.handle, k, buf.ctypes.data_as(ctypes.c_char_p), 64))
+    assert bytes(buf).split(b"\0")[0].decode() == want
+    S, seed, begin = 3000, 7, 5550001
+    rejects = np.zeros(S, np.uint32)
+    rc, opanels, oatt, _ = coracle.draw(o, k, seed, begin, S, max_attempts=100000, rejects=rejects)
+    A.draw_stats(enc, reset=True)
+    panels, attempts = _sample(enc, k, S, seed, begin, max_attempts=100000)
+    stats = A.draw_stats(enc)
+    assert rc == 0
+    assert np.array_equal(attempts, oatt)
+    assert np.array_equal(panels, opanels)
+    assert stats == {"attempts": int(oatt.sum()), "rejections": int(rejects.sum()),
+                     "selection_errors": int(oatt.sum()) - S - int(rejects.sum())}
