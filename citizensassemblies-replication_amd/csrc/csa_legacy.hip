@@ -2684,8 +2684,12 @@ struct PairPlan {
     int npad, nbt, ntri, nsplit;
 };
 
-// one 512-thread workgroup per CU (two waves per SIMD): fill the CUs once, keep >= 8 panel
-// blocks per split, and keep every split below the accumulator's exact range (f32: 2^24)
+// one 512-thread workgroup per CU (two waves per SIMD).  Splits of the panel blocks: the smallest count
+// whose rounds of CU-wide workgroups, each 1/ns of a tile, come within 2 % of the best balance over
+// ns <= 64 (ntri <= cus / 2: the CUs filled once, ns = cus / ntri as before -- sf_e 28 tiles x 9,
+// n = 2000 36 x 7; 128 < ntri < 256: one split left up to half the CUs idle, n = 4096's 136 tiles
+// 5.0 ms per 10^6 panels -- 15 splits make 8 rounds of 1/15 tile).  At least 8 panel blocks per
+// split, and every split below the accumulator's exact range (f32: 2^24).
 int pair_plan(int32_t n, uint64_t n_blocks, uint32_t engine, PairPlan &p) {
     if (engine != CSA_PAIR_FP4 && engine != CSA_PAIR_I8) return fail(CSA_E_INVALID, "pairs: unknown engine %u", engine);
     p.npad = csa_xt_pad(n);
@@ -2694,8 +2698,17 @@ int pair_plan(int32_t n, uint64_t n_blocks, uint32_t engine, PairPlan &p) {
     int cus = 256;
     int dev = 0;
     if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    const uint64_t ns_cap = std::max<uint64_t>(1, n_blocks / 8);
     uint64_t ns = std::max(1, cus / p.ntri);
-    ns = std::min<uint64_t>(ns, std::max<uint64_t>(1, n_blocks / 8));
+    if (2 * p.ntri > cus) {  // time per split-round layout ~ ceil(ntri ns / cus) / ns
+        auto cost = [&](uint64_t m) { return (double)((p.ntri * m + cus - 1) / cus) / (double)m; };
+        const uint64_t hi = std::min<uint64_t>(64, ns_cap);
+        double best = cost(1);
+        for (uint64_t m = 2; m <= hi; ++m) best = std::min(best, cost(m));
+        ns = 1;
+        while (ns < hi && cost(ns) > 1.02 * best) ++ns;
+    }
+    ns = std::min<uint64_t>(ns, ns_cap);
     const uint64_t exact_blocks = engine == CSA_PAIR_FP4 ? (1ull << 24) / 64 : (1ull << 31) / 64;
     ns = std::max<uint64_t>(ns, (n_blocks + exact_blocks - 1) / exact_blocks);
     if (ns > (1u << 20)) return fail(CSA_E_UNSUPPORTED, "pairs: too many panel blocks per call");

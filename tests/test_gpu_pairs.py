@@ -134,17 +134,19 @@ def test_pair_fp4_exact_beyond_f32_range(gpu_available):
     assert int(P[2, 3]) == 0 and int(P[0, 2]) == 0
 
 
+@pytest.mark.parametrize("n", [8192, 4096, 4500])
 @pytest.mark.parametrize("engine", [0, 1])
-def test_pairs_n8192_vs_torch_fp32(gpu_available, pair_kernel, engine):
+def test_pairs_n8192_vs_torch_fp32(gpu_available, pair_kernel, engine, n):
     """BASELINE config 5 shape: n = 8192 (32 triangle rows of 256 x 256 blocks), S = 131072 panels of
     ~2.5 % density (k ~ 200), against a plain PyTorch fp32 X^T X on the device (rocBLAS; exact:
-    every partial sum <= S < 2^24, and gfx950 has no reduced-precision fp32 GEMM mode)."""
+    every partial sum <= S < 2^24, and gfx950 has no reduced-precision fp32 GEMM mode).  n = 4096 / 4500
+    (136 / 171 tiles, fewer than the CUs): the split kernel's balanced split counts (13 / 19)."""
     import torch
     N = pkg("_native")
-    n, S = 8192, 131072
+    S = 131072
     npad = int(N.lib().csa_xt_pad(n))
     nblk = S // 64
-    g = torch.Generator(device="cuda").manual_seed(8192 + engine)
+    g = torch.Generator(device="cuda").manual_seed(n + engine)
     X = (torch.rand(S, n, device="cuda", generator=g) < 0.025)
     X[:, 17] = True                                              # a dense agent: counts up to S
     # pack the transposed bits: xt[b, p] bit j = X[64 b + j, p]
