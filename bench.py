@@ -379,8 +379,10 @@ def main():
         if e:
             e[1].record(stream)
         if want_pairs:
-            # the pair matrix is stored (overwrite), not zero-filled and added
-            pipe.pair_counts(S, overwrite=True)
+            # the pair matrix is stored (overwrite), not zero-filled and added; with the draws of the
+            # next steps in flight on the other stream the per-CU pair kernel takes its 256-register
+            # form, which leaves room for a draw workgroup beside it
+            pipe.pair_counts(S, overwrite=True, shared=overlap)
         if e:
             e[2].record(stream)
         if world == 1:

@@ -987,7 +987,15 @@ constexpr uint64_t kP2MaxBlocks = ((1ull << 24) - 1) / 64;  // whole-tile items 
 
 struct PairMap {
     int nbt, ntri, P;   // tiles per side, upper-triangle tiles, workgroups per XCD
+    int halves;         // work items per tile: 1 (256 x 256 items) or 2 (256 x 128 column halves)
     uint64_t nblk;      // 64-panel blocks
+    __host__ __device__ int nitems() const { return ntri * halves; }
+    // item idx = (tile idx / halves in locality order, column half idx % halves): its tile and the
+    // first column of the half inside it
+    __host__ __device__ void item_at(int idx, int &bi, int &bj, int &c0) const {
+        tile_at(idx / halves, bi, bj);
+        c0 = (idx % halves) * (kPairBlock / halves);
+    }
     // tile at locality-order index idx
     __host__ __device__ void tile_at(int idx, int &bi, int &bj) const {
         int r0 = 0;
@@ -1015,8 +1023,8 @@ struct PairMap {
         }
     }
     __host__ __device__ void xcd_chunk(int x, int &t0, int &tx) const {
-        t0 = (int)((int64_t)ntri * x / kP2Xcds);
-        tx = (int)((int64_t)ntri * (x + 1) / kP2Xcds) - t0;
+        t0 = (int)((int64_t)nitems() * x / kP2Xcds);
+        tx = (int)((int64_t)nitems() * (x + 1) / kP2Xcds) - t0;
     }
     // leftover tiles (the last tx mod P of each XCD chunk) pooled over the XCDs: their number, the
     // k-pieces per tile (every workgroup takes at most one piece), and the tile of pooled index l
@@ -1044,23 +1052,43 @@ struct PairMap {
 typedef __attribute__((address_space(3))) void lds_void_t;
 typedef const __attribute__((address_space(1))) void gbl_void_t;
 
-// MODE 0: one barrier per block; 1: one per two blocks; 2: one per block with the fragments of block
-// j + 1 expanded while block j's MFMAs run (raw words two blocks ahead)
-template <int MODE>
-__global__ __launch_bounds__(kP2Threads, 1) void pair_fp4_tile_kernel(const uint32_t *__restrict__ xt, int n,
-                                                                       int npad, PairMap M,
-                                                                       int64_t *__restrict__ pairs,
-                                                                       int32_t *__restrict__ part, int overwrite) {
-    __shared__ uint32_t ring[kP2Depth][4][kPairBlock];  // slot: A plane 0, A plane 1, B plane 0, B plane 1
+// NB = B fragments per wave.  NB = 4: 128 x 128 wave tiles, 256 x 256 items, 256 accumulators (one
+// wave fills its SIMD's 512 registers).  NB = 2 (CSA_PAIR_SHARED): 128 x 64 wave tiles, 256 x 128 items
+// (the column halves of a tile, PairMap::halves = 2), 128 accumulators, at most 256 registers -- a draw
+// workgroup's two 128-VGPR waves per SIMD fit beside it.
+// Every wave streams its own operands -- its 128 A rows and 32 NB B columns of each 64-panel block, two
+// LDS-DMAs (global_load_lds_dwordx4, 1 KiB each) into a private ring of kP2Depth 2 KiB slots -- so no
+// wave ever waits for another: no workgroup barrier in the block loop (a shared ring with one barrier
+// per block ran 10.4 / 14.8 ms vs 10.3 / 13.3 ms per 10^6 panels at n = 8192, NB = 4 / 2).  The A and B
+// strips are fetched twice per workgroup (once per wave row / column); the second fetch hits L2.
+// Step j waits for its own block j + 2 (vmcnt: blocks j + 3 .. j + D - 1, two DMAs each, may still be in
+// flight), issues block j + D into the slot block j leaves (read in step j - 2, whose ds_reads the
+// lgkmcnt(0) of step j - 1 retired), reads block j + 2's words, expands block j + 1's fragments (VALU
+// interleaved with block j's MFMAs) and runs block j's MFMAs.  The DMA issue is branch-free (past the
+// last block it re-loads the last block into a slot nobody reads), so the counted waits are constants.
+template <int NB>
+__global__ __launch_bounds__(kP2Threads, NB == 4 ? 1 : 2) void pair_fp4_tile_kernel(const uint32_t *__restrict__ xt,
+                                                                                  int n, int npad, PairMap M,
+                                                                                  int64_t *__restrict__ pairs,
+                                                                                  int32_t *__restrict__ part,
+                                                                                  int overwrite) {
+    static_assert(NB == 2 || NB == 4, "B fragments per wave: 2 or 4");
+    constexpr int BC = 32 * NB;  // B columns of a wave
+    // slot (u32): A plane 0 rows 0..127, A plane 1, B plane 0 columns 0..BC-1, B plane 1, padding
+    __shared__ uint32_t ring[4][kP2Depth][512];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int wr = wave >> 1, wc = wave & 1, r32 = lane & 31, h = lane >> 5;
     const int x = (int)blockIdx.x % kP2Xcds, w = (int)blockIdx.x / kP2Xcds;
     int t0, tx;
     M.xcd_chunk(x, t0, tx);
-    // whole tiles of this XCD's chunk, round r = tiles t0 + r P .. (its 32 workgroups together), then
-    // at most one k-piece of a pooled leftover tile (piece g of tile g / sp for workgroup g)
     const int F = tx / M.P, tl = M.leftovers(), sp = M.pieces(tl), g = (int)blockIdx.x;
     const int items = F + (g < tl * sp ? 1 : 0);
+    // DMA lanes: A chunk = lane (plane lane / 32, rows 4 (lane % 32) ..); B chunk = lane % (BC / 2)
+    // (plane .. / (BC / 4)); at NB = 2 lanes 32..63 repeat lanes 0..31 into the slot's padding
+    const int bl = lane % (BC / 2);
+    const int offa = (lane >> 5) * npad + 128 * wr + 4 * (lane & 31);
+    const int offb = (bl / (BC / 4)) * npad + BC * wc + 4 * (bl % (BC / 4));
+    uint32_t(&myring)[kP2Depth][512] = ring[wave];
     for (int it = 0; it < items; ++it) {
         int idx, slot = -1;
         uint64_t kb0 = 0, kb1 = M.nblk;
@@ -1073,187 +1101,85 @@ __global__ __launch_bounds__(kP2Threads, 1) void pair_fp4_tile_kernel(const uint
             kb1 = M.nblk * (uint64_t)(q + 1) / (uint64_t)sp;
             slot = g;
         }
-        int bi, bj;
-        M.tile_at(idx, bi, bj);
-        const int I0 = bi * kPairBlock, J0 = bj * kPairBlock;
-        v16f acc[4][4];
+        int bi, bj, c0;
+        M.item_at(idx, bi, bj, c0);
+        const int I0 = bi * kPairBlock, J0 = bj * kPairBlock + c0;
+        v16f acc[4][NB];
 #pragma unroll
         for (int a = 0; a < 4; ++a)
 #pragma unroll
-            for (int b = 0; b < 4; ++b)
+            for (int b = 0; b < NB; ++b)
 #pragma unroll
                 for (int v = 0; v < 16; ++v) acc[a][b][v] = 0.0f;
-        // this wave's DMA piece of every block: plane (wave & 1) of the A (waves 0, 1) or B strip
-        const uint32_t *gsrc = xt + (uint64_t)(wave & 1) * npad + (wave < 2 ? I0 : J0) + 4 * lane;
-        asm volatile("" : "+v"(gsrc));
-        const int nb = (int)(kb1 - kb0);  // <= kP2MaxBlocks
-        const uint32_t *gblk = gsrc + 2 * kb0 * (uint64_t)npad;
         const uint64_t bstride = 2 * (uint64_t)npad;
-        // every DMA of the previous item has landed (ring slots are refilled below) and every wave is
-        // done reading the ring
+        const uint32_t *ga = xt + 2 * kb0 * (uint64_t)npad + I0 + offa;
+        const uint32_t *gb = xt + 2 * kb0 * (uint64_t)npad + J0 + offb;
+        asm volatile("" : "+v"(ga), "+v"(gb));
+        const int nb = (int)(kb1 - kb0);  // <= kP2MaxBlocks
+        // the previous item's trailing DMAs (re-loads of its last block) have landed
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        // Branch-free pipeline: every step issues exactly one DMA per wave (past the last block it
-        // re-loads the last block into a slot nobody reads again), so the counted waits are constant:
-        // before step j, D + j pieces were issued and block j + 1 is the (j + 2)-th -> vmcnt(D - 2).
-        auto dma = [&](int blk, int slot) {
-            __builtin_amdgcn_global_load_lds((gbl_void_t *)(gblk + (uint64_t)min(blk, nb - 1) * bstride),
-                                             (lds_void_t *)&ring[slot][wave][0], 16, 0, 0);
+        auto dma = [&](int blk, int sl) {
+            const uint64_t o = (uint64_t)min(blk, nb - 1) * bstride;
+            __builtin_amdgcn_global_load_lds((gbl_void_t *)(ga + o), (lds_void_t *)&myring[sl][0], 16, 0, 0);
+            __builtin_amdgcn_global_load_lds((gbl_void_t *)(gb + o), (lds_void_t *)&myring[sl][256], 16, 0, 0);
         };
-        auto compute = [&](const uint32_t(&ca)[4], const uint32_t(&cb)[4]) {
-            v8i fa[4], fb[4];
+        static_assert((kP2Depth & (kP2Depth - 1)) == 0 && kP2Depth >= 4, "ring slots: power of two >= 4");
+        auto read_blk = [&](int blk, uint32_t(&na)[4], uint32_t(&nbw)[NB]) {
+            const uint32_t *sl = myring[blk & (kP2Depth - 1)];
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                fa[q] = f4_frag_a(ca[q]);
-                fb[q] = f4_frag_b(cb[q]);
-            }
+            for (int q = 0; q < 4; ++q) na[q] = sl[128 * h + 32 * q + r32];
+#pragma unroll
+            for (int q = 0; q < NB; ++q) nbw[q] = sl[256 + BC * h + 32 * q + r32];
+        };
+        auto expand = [&](const uint32_t(&ca)[4], const uint32_t(&cb)[NB], v8i(&fa)[4], v8i(&fb)[NB]) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) fa[q] = f4_frag_a(ca[q]);
+#pragma unroll
+            for (int q = 0; q < NB; ++q) fb[q] = f4_frag_b(cb[q]);
+        };
+        auto mfma = [&](const v8i(&fa)[4], const v8i(&fb)[NB]) {
 #pragma unroll
             for (int a = 0; a < 4; ++a)
 #pragma unroll
-                for (int b = 0; b < 4; ++b)
+                for (int b = 0; b < NB; ++b)
                     acc[a][b] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(fa[a], fb[b], acc[a][b], 4, 4, 0,
                                                                                 0x7F7F7F7F, 0, 0x7F7F7F7F);
         };
-        static_assert((kP2Depth & (kP2Depth - 1)) == 0 && kP2Depth >= 4, "ring slots: power of two >= 4");
-        auto read_blk = [&](int blk, uint32_t(&na)[4], uint32_t(&nbw)[4]) {
-            const int sl = blk & (kP2Depth - 1);
+        if (nb > 0) {
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                na[q] = ring[sl][h][128 * wr + 32 * q + r32];
-                nbw[q] = ring[sl][2 + h][128 * wc + 32 * q + r32];
-            }
-        };
-        if constexpr (MODE == 0) {
-            // one barrier per block: block j + 1 readable (this wave's piece by the counted wait, the
-            // others' by the barrier, which also retires every wave's reads of block j, whose slot
-            // then takes block j + D), its words read while block j's MFMAs run.  Before step j,
-            // D + j pieces were issued and block j + 1 is the (j + 2)-th -> vmcnt(D - 2).
-            auto step = [&](int j, const uint32_t(&ca)[4], const uint32_t(&cb)[4], uint32_t(&na)[4],
-                            uint32_t(&nbw)[4]) {
-                __builtin_amdgcn_sched_barrier(0);  // the previous block's MFMAs stay ahead of this barrier
-                asm volatile("s_waitcnt lgkmcnt(0)\n\ts_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(kP2Depth - 2) : "memory");
+            for (int j = 0; j < kP2Depth; ++j) dma(j, j);
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * (kP2Depth - 2)) : "memory");
+            uint32_t r0a[4], r0b[NB], r1a[4], r1b[NB];
+            v8i f0a[4], f0b[NB], f1a[4], f1b[NB];
+            read_blk(0, r0a, r0b);
+            read_blk(1, r1a, r1b);
+            expand(r0a, r0b, f0a, f0b);
+            auto step = [&](int j, const v8i(&fca)[4], const v8i(&fcb)[NB], const uint32_t(&rna)[4],
+                            const uint32_t(&rnb)[NB], v8i(&fna)[4], v8i(&fnb)[NB], uint32_t(&rwa)[4],
+                            uint32_t(&rwb)[NB]) {
+                __builtin_amdgcn_sched_barrier(0);
+                asm volatile("s_waitcnt lgkmcnt(0)\n\ts_waitcnt vmcnt(%0)" ::"n"(2 * (kP2Depth - 3)) : "memory");
                 dma(j + kP2Depth, j & (kP2Depth - 1));
-                read_blk(j + 1, na, nbw);
-                compute(ca, cb);
+                read_blk(j + 2, rwa, rwb);
+                expand(rna, rnb, fna, fnb);
+                mfma(fca, fcb);
+                __builtin_amdgcn_sched_barrier(0);
             };
-            if (nb > 0) {
-#pragma unroll
-                for (int j = 0; j < kP2Depth; ++j) dma(j, j);
-                asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(kP2Depth - 1) : "memory");
-                uint32_t ra[4], rb[4], sa[4], sb[4];
-                read_blk(0, ra, rb);
-                int j = 0;
-                for (; j + 2 < nb; j += 2) {
-                    step(j, ra, rb, sa, sb);
-                    step(j + 1, sa, sb, ra, rb);
-                }
-                if (j + 1 < nb) {
-                    step(j, ra, rb, sa, sb);
-                    __builtin_amdgcn_sched_barrier(0);
-                    compute(sa, sb);
-                } else {
-                    compute(ra, rb);
-                }
+            int j = 0;
+            for (; j + 2 <= nb; j += 2) {
+                step(j, f0a, f0b, r1a, r1b, f1a, f1b, r0a, r0b);
+                step(j + 1, f1a, f1b, r0a, r0b, f0a, f0b, r1a, r1b);
             }
-        } else if constexpr (MODE == 2) {
-            // Raw words two blocks ahead, fragments one block ahead: step j waits for block j + 2
-            // (this wave's piece: vmcnt; the others': the barrier, which also retires every read of
-            // block j, whose slot takes block j + D), reads block j + 2's words, expands block j + 1's
-            // (VALU interleaved with block j's MFMAs, so the next step's first MFMA does not wait on
-            // its fragments) and runs block j's MFMAs.  Before step j, D + j pieces were issued and
-            // block j + 2 is the (j + 3)-th -> vmcnt(D - 3).
-            auto expand = [&](const uint32_t(&ca)[4], const uint32_t(&cb)[4], v8i(&fa)[4], v8i(&fb)[4]) {
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    fa[q] = f4_frag_a(ca[q]);
-                    fb[q] = f4_frag_b(cb[q]);
-                }
-            };
-            auto mfma = [&](const v8i(&fa)[4], const v8i(&fb)[4]) {
-#pragma unroll
-                for (int a = 0; a < 4; ++a)
-#pragma unroll
-                    for (int b = 0; b < 4; ++b)
-                        acc[a][b] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(fa[a], fb[b], acc[a][b], 4, 4, 0,
-                                                                                    0x7F7F7F7F, 0, 0x7F7F7F7F);
-            };
-            if (nb > 0) {
-#pragma unroll
-                for (int j = 0; j < kP2Depth; ++j) dma(j, j);
-                asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(kP2Depth - 2) : "memory");
-                uint32_t r0a[4], r0b[4], r1a[4], r1b[4];
-                v8i f0a[4], f0b[4], f1a[4], f1b[4];
-                read_blk(0, r0a, r0b);
-                read_blk(1, r1a, r1b);
-                expand(r0a, r0b, f0a, f0b);
-                auto step = [&](int j, const v8i(&fca)[4], const v8i(&fcb)[4], const uint32_t(&rna)[4],
-                                const uint32_t(&rnb)[4], v8i(&fna)[4], v8i(&fnb)[4], uint32_t(&rwa)[4],
-                                uint32_t(&rwb)[4]) {
-                    __builtin_amdgcn_sched_barrier(0);
-                    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(kP2Depth - 3) : "memory");
-                    dma(j + kP2Depth, j & (kP2Depth - 1));
-                    read_blk(j + 2, rwa, rwb);
-                    expand(rna, rnb, fna, fnb);
-                    mfma(fca, fcb);
-                };
-                // (the spill slots of this kernel -- 58 VGPRs at MODE 2 -- are written and read in the
-                // prologue, the odd-block tail and the epilogue, once per item; the block loop has none.
-                // A wave-uniform skip of the last pair's second step inside the loop instead of this
-                // tail put 102 spill slots into the loop.)
-                int j = 0;
-                for (; j + 2 <= nb; j += 2) {
-                    step(j, f0a, f0b, r1a, r1b, f1a, f1b, r0a, r0b);
-                    step(j + 1, f1a, f1b, r0a, r0b, f0a, f0b, r1a, r1b);
-                }
-                if (j < nb) step(j, f0a, f0b, r1a, r1b, f1a, f1b, r0a, r0b);
-            }
-        } else {
-            // one barrier per two blocks: at even j it makes blocks j + 1 and j + 2 readable and retires
-            // every read of blocks j - 1 and j, whose slots take blocks j + D - 1 and j + D.  The
-            // prologue issues D - 1 pieces, each even step two more: before even step j, D - 1 + j were
-            // issued and block j + 2 is the (j + 3)-th -> vmcnt(D - 4).  Odd steps only read and compute.
-            if (nb > 0) {
-#pragma unroll
-                for (int j = 0; j < kP2Depth - 1; ++j) dma(j, j);
-                asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(kP2Depth - 2) : "memory");
-                uint32_t ra[4], rb[4], sa[4], sb[4];
-                read_blk(0, ra, rb);
-                auto even = [&](int j) {  // computes block j (ra, rb), reads block j + 1 into (sa, sb)
-                    __builtin_amdgcn_sched_barrier(0);
-                    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(kP2Depth - 4) : "memory");
-                    dma(j + kP2Depth - 1, (j - 1) & (kP2Depth - 1));
-                    dma(j + kP2Depth, j & (kP2Depth - 1));
-                    read_blk(j + 1, sa, sb);
-                    compute(ra, rb);
-                };
-                int j = 0;
-                for (; j + 2 < nb; j += 2) {
-                    even(j);
-                    __builtin_amdgcn_sched_barrier(0);
-                    read_blk(j + 2, ra, rb);  // landed by the even barrier
-                    compute(sa, sb);
-                }
-                if (j + 1 < nb) {
-                    even(j);
-                    __builtin_amdgcn_sched_barrier(0);
-                    compute(sa, sb);
-                } else {
-                    compute(ra, rb);
-                }
-            }
+            if (j < nb) step(j, f0a, f0b, r1a, r1b, f1a, f1b, r0a, r0b);
         }
-        // C/D layout: col = lane & 31, row = (v & 3) + 8 (v >> 2) + 4 (lane >> 5).  The lane offsets
-        // are laundered through an empty asm so that the compiler does not hoist the 256 store
-        // addresses of the epilogue out of the item loop (they spilled, and the spill traffic
-        // shares vmcnt with the LDS-DMA pipeline)
-        int rloc = 128 * wr + 4 * h, cloc = 128 * wc + r32;
+        int rloc = 128 * wr + 4 * h, cloc = BC * wc + r32;
         asm volatile("" : "+v"(rloc), "+v"(cloc));
         if (slot >= 0) {
             int32_t *dst = part + (size_t)slot * kPairBlock * kPairBlock;
 #pragma unroll
             for (int a = 0; a < 4; ++a)
 #pragma unroll
-                for (int b = 0; b < 4; ++b)
+                for (int b = 0; b < NB; ++b)
 #pragma unroll
                     for (int v = 0; v < 16; ++v)
                         dst[(rloc + 32 * a + (v & 3) + 8 * (v >> 2)) * kPairBlock + cloc + 32 * b] = (int)acc[a][b][v];
@@ -1261,7 +1187,7 @@ __global__ __launch_bounds__(kP2Threads, 1) void pair_fp4_tile_kernel(const uint
 #pragma unroll
             for (int a = 0; a < 4; ++a)
 #pragma unroll
-                for (int b = 0; b < 4; ++b) {
+                for (int b = 0; b < NB; ++b) {
                     const int col = J0 + cloc + 32 * b;
 #pragma unroll
                     for (int v = 0; v < 16; ++v) {
@@ -1277,16 +1203,16 @@ __global__ __launch_bounds__(kP2Threads, 1) void pair_fp4_tile_kernel(const uint
     }
 }
 
-// Sums the k-pieces of the pooled leftover tiles of pair_fp4_tile_kernel (piece q of leftover tile l
-// in partial slot l * sp + q) into the int64 output: block (row, l) = row `row` of leftover tile l.
+// Sums the k-pieces of the pooled leftover items of pair_fp4_tile_kernel (piece q of leftover item l
+// in partial slot l * sp + q) into the int64 output: block (row, l) = row `row` of leftover item l.
 __global__ __launch_bounds__(kPairBlock) void pair_reduce2_kernel(const int32_t *__restrict__ part, int n, PairMap M,
                                                                  int64_t *__restrict__ pairs, int overwrite) {
     const int l = (int)blockIdx.y, sp = M.pieces(M.leftovers());
-    int bi, bj;
-    M.tile_at(M.leftover_tile(l), bi, bj);
+    int bi, bj, c0;
+    M.item_at(M.leftover_tile(l), bi, bj, c0);
     const int r = (int)blockIdx.x, c = (int)threadIdx.x;
-    const int row = bi * kPairBlock + r, col = bj * kPairBlock + c;
-    if (row >= n || col >= n) return;
+    const int row = bi * kPairBlock + r, col = bj * kPairBlock + c0 + c;
+    if (c >= kPairBlock / M.halves || row >= n || col >= n) return;
     const int32_t *p = part + (size_t)(l * sp) * kPairBlock * kPairBlock + r * kPairBlock + c;
     int64_t acc = 0;
     for (int q = 0; q < sp; ++q) acc += p[(size_t)q * kPairBlock * kPairBlock];
@@ -2167,7 +2093,7 @@ int launch_draw(const csa_instance *I, int32_t k, uint64_t seed, uint64_t panel_
         const char *e = getenv("CSA_DRAW_LDS_PAD");
         return e ? (size_t)strtoull(e, nullptr, 10) : (size_t)0;
     }();
-    const size_t lds_launch = (cfg.lane || cfg.solo) && lds + lds_pad <= 160 * 1024 ? lds + lds_pad : lds;
+    const size_t lds_launch = (cfg.lane || cfg.solo || cfg.wide) && lds + lds_pad <= 160 * 1024 ? lds + lds_pad : lds;
     const uint64_t want = (n_panels + groups_wg - 1) / groups_wg;
     // the lane kernel: one workgroup per 128 panels, not persistent -- sf_e 10^6 panels: 4.47 ms vs
     // 5.05 ms for a persistent grid, and retiring workgroups let a concurrent stream's kernels in.
@@ -2728,7 +2654,7 @@ struct Pair2Plan {
     int grid = 0, lmax = 0;  // persistent workgroups; leftover tiles (pooled over the XCDs)
 };
 
-bool pair2_plan(int32_t n, uint64_t n_blocks, uint32_t engine, Pair2Plan &q) {
+bool pair2_plan(int32_t n, uint64_t n_blocks, uint32_t engine, bool shared, Pair2Plan &q) {
     if (engine != CSA_PAIR_FP4 || n_blocks == 0 || n_blocks > kP2MaxBlocks) return false;
     const char *e = getenv("CSA_PAIR_KERNEL");
     const int force = e ? atoi(e) : 0;
@@ -2736,6 +2662,11 @@ bool pair2_plan(int32_t n, uint64_t n_blocks, uint32_t engine, Pair2Plan &q) {
     int cus = 256, dev = 0;
     if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     if (cus < kP2Xcds || cus % kP2Xcds) return false;
+    // B fragments per wave: 2 (256-register waves) when the launch shares the CUs with draws
+    // (CSA_PAIR_SHARED), else 4; CSA_P2_NB=2|4 forces either (A/B)
+    const char *enb = getenv("CSA_P2_NB");
+    const int nbf = enb ? atoi(enb) : (shared ? 2 : 4);
+    q.M.halves = nbf == 2 ? 2 : 1;
     q.M.nbt = csa_xt_pad(n) / kPairBlock;
     q.M.ntri = q.M.nbt * (q.M.nbt + 1) / 2;
     q.M.P = cus / kP2Xcds;
@@ -2751,10 +2682,13 @@ uint64_t pair2_scratch_bytes(const Pair2Plan &q) {
 }  // namespace
 
 uint64_t csa_pair_scratch_bytes(int32_t n, uint64_t n_blocks, uint32_t engine) {
-    engine &= ~CSA_PAIR_OVERWRITE;
+    engine &= ~(CSA_PAIR_OVERWRITE | CSA_PAIR_SHARED);
     if (n <= 0 || n_blocks == 0) return 0;
-    Pair2Plan q;
-    if (pair2_plan(n, n_blocks, engine, q)) return std::max<uint64_t>(pair2_scratch_bytes(q), 4);
+    // enough for either form of the per-CU kernel, so one buffer serves calls with and without
+    // CSA_PAIR_SHARED
+    Pair2Plan q, q2;
+    if (pair2_plan(n, n_blocks, engine, false, q) && pair2_plan(n, n_blocks, engine, true, q2))
+        return std::max<uint64_t>(std::max(pair2_scratch_bytes(q), pair2_scratch_bytes(q2)), 4);
     PairPlan p;
     if (pair_plan(n, n_blocks, engine, p)) return 0;
     return (uint64_t)p.ntri * p.nsplit * kPairBlock * kPairBlock * sizeof(int32_t);
@@ -2763,26 +2697,22 @@ uint64_t csa_pair_scratch_bytes(int32_t n, uint64_t n_blocks, uint32_t engine) {
 int csa_pair_counts_ex_async(const uint64_t *d_xt, uint64_t n_blocks, int32_t n, int64_t *d_pairs,
                              uint32_t engine, void *d_scratch, uint64_t scratch_bytes, void *stream) {
     if (n <= 0 || !d_xt || !d_pairs) return fail(CSA_E_INVALID, "pairs: bad arguments");
-    const bool overwrite = (engine & CSA_PAIR_OVERWRITE) != 0u;
-    engine &= ~CSA_PAIR_OVERWRITE;
+    const bool overwrite = (engine & CSA_PAIR_OVERWRITE) != 0u, shared = (engine & CSA_PAIR_SHARED) != 0u;
+    engine &= ~(CSA_PAIR_OVERWRITE | CSA_PAIR_SHARED);
     const hipStream_t st = (hipStream_t)stream;
     if (overwrite && (n_blocks == 0 || !d_scratch))  // no reduce pass to store every element
         HIPCHK(hipMemsetAsync(d_pairs, 0, (size_t)n * n * sizeof(int64_t), st));
     if (n_blocks == 0) return CSA_OK;
     Pair2Plan q;
-    if (d_scratch && pair2_plan(n, n_blocks, engine, q)) {
+    if (d_scratch && pair2_plan(n, n_blocks, engine, shared, q)) {
         if (scratch_bytes < pair2_scratch_bytes(q))
             return fail(CSA_E_INVALID, "pairs: scratch of %llu B < csa_pair_scratch_bytes = %llu B",
                         (unsigned long long)scratch_bytes, (unsigned long long)pair2_scratch_bytes(q));
         int32_t *part = static_cast<int32_t *>(d_scratch);
         const uint32_t *xt32 = reinterpret_cast<const uint32_t *>(d_xt);
         const int npad = csa_xt_pad(n), ow = overwrite ? 1 : 0;
-        // CSA_P2_MODE=0|1|2 selects the pipeline variant (A/B); default 2
-        const char *pm = getenv("CSA_P2_MODE");
-        const int mode = pm ? atoi(pm) : 2;
-        const void *fn = mode == 0   ? reinterpret_cast<const void *>(&pair_fp4_tile_kernel<0>)
-                         : mode == 1 ? reinterpret_cast<const void *>(&pair_fp4_tile_kernel<1>)
-                                     : reinterpret_cast<const void *>(&pair_fp4_tile_kernel<2>);
+        const void *fn = q.M.halves == 2 ? reinterpret_cast<const void *>(&pair_fp4_tile_kernel<2>)
+                                         : reinterpret_cast<const void *>(&pair_fp4_tile_kernel<4>);
         PairMap M = q.M;
         void *args[] = {(void *)&xt32, &n, (void *)&npad, &M, &d_pairs, &part, (void *)&ow};
         HIPCHK(hipLaunchKernel(fn, dim3(q.grid), dim3(kP2Threads), args, 0, st));

@@ -247,10 +247,15 @@ int csa_transpose_count_async(const uint64_t *d_panels, uint64_t n_panels, int32
  * accumulating: on return d_pairs holds exactly this batch's counts for i <= j
  * (the reduce kernel writes every element of the upper-triangular blocks; without
  * scratch the call zero-fills d_pairs first), so a caller that counts each batch
- * afresh needs no n*n zero-fill of its own. */
+ * afresh needs no n*n zero-fill of its own.  engine | CSA_PAIR_SHARED is a
+ * scheduling hint, never a change of result: the launch will share the CUs with
+ * concurrent draw kernels (a pipelined caller), so the per-CU kernel takes its
+ * 256-register form (128 x 64 wave tiles) that leaves room for a draw workgroup
+ * beside it, instead of the 512-register form that is faster alone. */
 #define CSA_PAIR_FP4 0u
 #define CSA_PAIR_I8 1u
 #define CSA_PAIR_OVERWRITE 0x100u
+#define CSA_PAIR_SHARED 0x200u
 uint64_t csa_pair_scratch_bytes(int32_t n, uint64_t n_blocks, uint32_t engine);
 int csa_pair_counts_ex_async(const uint64_t *d_xt, uint64_t n_blocks, int32_t n, int64_t *d_pairs,
                              uint32_t engine, void *d_scratch, uint64_t scratch_bytes, void *stream);

@@ -41,11 +41,14 @@ def _planes(w):
     return w.contiguous().view(torch.int32).view(nblk, npad, 2).permute(0, 2, 1).contiguous()
 
 
-@pytest.fixture(params=["tile", "split"])
+@pytest.fixture(params=["tile4", "tile2", "split"])
 def pair_kernel(request, monkeypatch):
-    """fp4 kernel: pair_fp4_tile_kernel (CSA_PAIR_KERNEL=2; the default from n ~ 5.7k on) or
-    pair_mfma_kernel (CSA_PAIR_KERNEL=1; the default below)."""
+    """fp4 kernel: pair_fp4_tile_kernel (CSA_PAIR_KERNEL=2; the default from n ~ 5.7k on) in its
+    512-register (NB = 4, alone) or 256-register (NB = 2, CSA_PAIR_SHARED) form, or pair_mfma_kernel
+    (CSA_PAIR_KERNEL=1; the default below)."""
     monkeypatch.setenv("CSA_PAIR_KERNEL", "1" if request.param == "split" else "2")
+    if request.param != "split":
+        monkeypatch.setenv("CSA_P2_NB", request.param[4:])
     return request.param
 
 
@@ -170,9 +173,11 @@ def test_pairs_n8192_vs_torch_fp32(gpu_available, pair_kernel, engine, n):
 
 @pytest.mark.parametrize("n,nblk", [(20, 1), (20, 31), (257, 3), (1727, 40), (4100, 7), (8192, 33)])
 @pytest.mark.parametrize("overwrite", [True, False])
-def test_pair_tile_kernel_small_and_ragged(gpu_available, monkeypatch, n, nblk, overwrite):
-    """pair_fp4_tile_kernel edge cases: fewer panel blocks than k-pieces (empty pieces), one tile only
-    (n = 20: one XCD has work), XCD chunks with and without leftover tiles, n not a multiple of 256."""
+@pytest.mark.parametrize("shared", [False, True])
+def test_pair_tile_kernel_small_and_ragged(gpu_available, monkeypatch, n, nblk, overwrite, shared):
+    """pair_fp4_tile_kernel edge cases, both forms (CSA_PAIR_SHARED: 256 x 128 column-half items): fewer
+    panel blocks than k-pieces (empty pieces), one tile only (n = 20: one XCD has work), XCD chunks with
+    and without leftover items, n not a multiple of 256, a column half wholly past n (n = 4100)."""
     monkeypatch.setenv("CSA_PAIR_KERNEL", "2")
     N = pkg("_native")
     npad = int(N.lib().csa_xt_pad(n))
@@ -182,6 +187,6 @@ def test_pair_tile_kernel_small_and_ragged(gpu_available, monkeypatch, n, nblk, 
     xt[:, n:] = 0
     ref = _cpu_pairs(xt, n, npad)
     iu = np.triu_indices(n)
-    engine = N.CSA_PAIR_FP4 | (N.CSA_PAIR_OVERWRITE if overwrite else 0)
+    engine = N.CSA_PAIR_FP4 | (N.CSA_PAIR_OVERWRITE if overwrite else 0) | (N.CSA_PAIR_SHARED if shared else 0)
     got = _run(xt, n, engine, True, init=-3)
     assert np.array_equal(got[iu], ref[iu] + (0 if overwrite else -3))

@@ -19,7 +19,7 @@ def main():
     ap.add_argument("--n", type=int, default=8192)
     ap.add_argument("--panels", type=int, default=10 ** 6)
     ap.add_argument("--reps", type=int, default=5)
-    ap.add_argument("--variants", default="tile0,tile1,tile2,split")
+    ap.add_argument("--variants", default="tile4,tile2,split")
     ap.add_argument("--engine", default="fp4", choices=("fp4", "i8"))
     ap.add_argument("--density", type=float, default=0.025)
     args = ap.parse_args()
@@ -43,12 +43,11 @@ def main():
     stream = torch.cuda.current_stream()
     out, ref = {}, None
     for var in args.variants.split(","):
-        # split = pair_mfma_kernel; tile<m> = pair_fp4_tile_kernel<m> (CSA_P2_MODE), tile = the default
+        # split = pair_mfma_kernel; tile<NB> = pair_fp4_tile_kernel<NB> (CSA_P2_NB); tile = the default
         os.environ["CSA_PAIR_KERNEL"] = "1" if var == "split" else "2"
+        os.environ.pop("CSA_P2_NB", None)
         if var.startswith("tile") and len(var) > 4:
-            os.environ["CSA_P2_MODE"] = var[4:]
-        else:
-            os.environ.pop("CSA_P2_MODE", None)
+            os.environ["CSA_P2_NB"] = var[4:]
         sb = int(L.csa_pair_scratch_bytes(n, nblk, engine))
         scr = torch.empty(max(sb, 4) // 4 + 1, dtype=torch.int32, device="cuda")
         pairs = torch.zeros(n * n, dtype=torch.int64, device="cuda")
