@@ -818,12 +818,15 @@ __global__ __launch_bounds__(kPairThreads) void pair_mfma_kernel(const uint64_t 
                                                                  int32_t *__restrict__ part) {
     __shared__ uint64_t words[2][KB][2 * kPairBlock];
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-    // consecutive workgroups (dispatched round-robin over the 8 XCDs) take the splits of one
-    // block; an XCD-grouped mapping (every workgroup of an XCD on one split, so the XT re-reads of
-    // that split stay in its L2) measured 0.90 vs 0.82 ms at sf_e: it needs nsplit % 8 == 0 and
-    // left 32 CUs idle
-    const int tri = (int)blockIdx.x / nsplit;
-    const int split = (int)blockIdx.x - tri * nsplit;
+    // Workgroup g runs on XCD g mod 8 (round-robin dispatch).  The (tile, split) items in
+    // split-major order are cut into 8 contiguous chunks, one per XCD, sized to that XCD's share of
+    // the grid: the ~32 workgroups of an XCD then cover one or two splits (their tiles share the
+    // split's XT strips through that XCD's L2) instead of every XCD touching every split -- sf_e
+    // (28 tiles x 9 splits) fetched 1.5 GB per launch for a 224 MB operand with the tile-major order.
+    // (Round 2's grouping of ONE split per XCD needed nsplit % 8 == 0 and left 32 CUs idle.)
+    const int g = (int)blockIdx.x, G = (int)gridDim.x, ntri = nbt * (nbt + 1) / 2;
+    const int xcd = g & 7, it = xcd * (G >> 3) + min(xcd, G & 7) + (g >> 3);
+    const int split = it / ntri, tri = it - split * ntri;
     const int item = tri * nsplit + split;
     int bi, bj;
     tri_block(tri, nbt, bi, bj);
