@@ -74,7 +74,24 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target duration of each CPU-baseline leg")
     ap.add_argument("--no-api", action="store_true", help="skip the legacy_probabilities end-to-end leg")
+    ap.add_argument("--job-panels", type=int, default=0,
+                    help="strong scaling (BASELINE configs 3 and 5): time ONE job of this many panels split "
+                         "over the N ranks (each rank's share in chunks of --panels; counts and pairs "
+                         "accumulated over the job, the exact distinct count over all of its panels); "
+                         "--steps is ignored, --warmup chunks of a throwaway job run first")
     return ap.parse_args()
+
+
+def digests(counts, pairs, n):
+    """SHA-256 of the final per-person count vector (int64, little-endian) and of the pair matrix's
+    upper triangle incl. the diagonal (np.triu of the int64 n x n matrix): equal digests at N = 1 and
+    N > 1 mean the whole vectors are equal, not just their sums."""
+    import numpy as np
+    out = {"counts_sha256": hashlib.sha256(np.ascontiguousarray(counts.cpu().numpy(), "<i8").tobytes()).hexdigest()}
+    if pairs is not None:
+        m = pairs.view(n, n).cpu().numpy()
+        out["pairs_triu_sha256"] = hashlib.sha256(np.ascontiguousarray(np.triu(m), "<i8").tobytes()).hexdigest()
+    return out
 
 
 def cpu_model():
@@ -246,10 +263,12 @@ def api_leg(P, A, inst, S, seed):
                                           "copied and divided on first access (pair_histogram_materialise_ms)"}
 
 
-def self_launch(n, script=None, argv=None):
+def self_launch(n, script=None, argv=None, grace=10.0):
     """`python bench.py --gpus N` without a launcher: start N rank processes of this same command
     (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set, one GPU each) and return the worst exit code.
-    Runs before anything imports torch or touches a device in this process."""
+    Runs before anything imports torch or touches a device in this process.  The ranks are polled:
+    when one exits non-zero the others (otherwise blocked in a rendezvous or collective until its
+    timeout) are terminated, then killed after ``grace`` seconds, and that first exit code returned."""
     import socket
     with socket.socket() as sk:
         sk.bind(("127.0.0.1", 0))
@@ -260,9 +279,146 @@ def self_launch(n, script=None, argv=None):
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         procs.append(subprocess.Popen([sys.executable, script or os.path.abspath(__file__)] +
                                       list(sys.argv[1:] if argv is None else argv), env=env))
-    rcs = [p.wait() for p in procs]
-    bad = [rc for rc in rcs if rc]
-    return max(bad, key=abs) if bad else 0
+    first_bad = 0
+    while True:
+        rcs = [p.poll() for p in procs]
+        bad = [rc for rc in rcs if rc]
+        if bad:
+            first_bad = bad[0]
+            break
+        if all(rc is not None for rc in rcs):
+            return 0
+        time.sleep(0.05)
+    for p in procs:               # a rank failed: the others would wait for it until their timeout
+        if p.poll() is None:
+            p.terminate()
+    deadline = time.time() + grace
+    for p in procs:
+        try:
+            p.wait(timeout=max(0.0, deadline - time.time()))
+        except subprocess.TimeoutExpired:
+            p.kill()
+            p.wait()
+    return first_bad
+
+
+def run_job(args, world, rank, dev, torch, dist, A, Dd, enc, k, S, inst_dir, pipe, want_pairs, stream, draw_name):
+    """--job-panels P: one whole job of P panels (global indices 0 .. P-1) split over the ranks in
+    contiguous shares (distributed.shard_range), every rank's share drawn in chunks of S panels.  All
+    draws are enqueued on the draw stream at once (each chunk has its own slice of the share's panel
+    buffer, so nothing waits for the counting), the counting stream follows chunk by chunk (counts and
+    pairs accumulate over the job), then the exact distinct count over the whole share (N = 1) or the
+    exchange of section 5 (N > 1: all_reduce of counts and packed pairs, 24-byte keys to the owners).
+    value = P / (the max over ranks of the barrier-to-barrier time of the whole job)."""
+    import ctypes
+    N = importlib.import_module(PKG + "._native")
+    Pj = int(args.job_panels)
+    b0, e0 = Dd.shard_range(Pj, world, rank)
+    share, n_max = e0 - b0, Dd.shard_range(Pj, world, 0)[1]
+    W = enc.W
+    draw_stream = torch.cuda.Stream(dev)
+    panels_all = torch.empty(max(share * W, 1), dtype=torch.int64, device=dev)
+    hashes_all = torch.empty(max(2 * share, 2), dtype=torch.int64, device=dev)
+    table = Dd.HashTable(max(share, 1), dev) if world == 1 else None
+    xchg = Dd.PanelExchange(n_max, W, world, dev, redraw=(enc.handle, k, args.seed, 0)
+                            if args.exchange == "keys" else None) if world > 1 else None
+
+    def job(begin, count):
+        steps = (count + S - 1) // S
+        with torch.cuda.stream(stream):
+            pipe.status.zero_()
+            pipe.counts.zero_()
+            if want_pairs and count == 0:
+                pipe.pairs.zero_()
+        drawn = []
+        for j in range(steps):
+            o, ln = j * S, min(S, count - j * S)
+            pipe.panels, pipe.hashes = panels_all[o * W:(o + ln) * W], hashes_all[2 * o:2 * (o + ln)]
+            pipe.draw(args.seed, begin + o, ln, stream=draw_stream)
+            ev = torch.cuda.Event()
+            ev.record(draw_stream)
+            drawn.append(ev)
+        for j in range(steps):
+            o, ln = j * S, min(S, count - j * S)
+            stream.wait_event(drawn[j])
+            pipe.panels, pipe.hashes = panels_all[o * W:(o + ln) * W], hashes_all[2 * o:2 * (o + ln)]
+            pipe.transpose_count(ln)
+            if want_pairs:
+                pipe.pair_counts(ln, overwrite=j == 0, shared=j + 1 < steps)
+        if world == 1:
+            table.ensure(count)
+            with torch.cuda.stream(stream):
+                table.count.zero_()
+            N.check(N.lib().csa_unique_async(N.ptr(hashes_all), N.ptr(panels_all), count, W, N.ptr(table.table),
+                                             table.slots, N.ptr(table.count), N.ptr(pipe.status),
+                                             ctypes.c_void_p(stream.cuda_stream)))
+            return table.count, steps
+        with torch.cuda.stream(stream):
+            _, _, u = Dd.combine(pipe.counts, pipe.pairs if want_pairs else None, hashes_all[: 2 * count],
+                                 panels_all[: count * W], W, exchange=xchg, stream=stream, pair_bound=Pj,
+                                 status=pipe.status, panel_begin=begin)
+        return u, steps
+
+    # warmup: a throwaway job of --warmup chunks on this rank's first panels
+    job(b0, min(share, args.warmup * S))
+    torch.cuda.synchronize()
+    pipe.check_status()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    A.draw_stats(enc, reset=True)
+    t0 = time.perf_counter()
+    u, steps = job(b0, share)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    pipe.check_status()
+    elapsed = t1 - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        st = torch.tensor([steps], dtype=torch.int64, device=dev)
+        dist.all_reduce(st, op=dist.ReduceOp.MAX)
+        steps = int(st.item())
+    checks = {"job_unique": int(u.item()), "job_count_sum": int(pipe.counts.sum().item()),
+              "job_pair_sum": int(torch.triu(pipe.pairs.view(enc.n, enc.n)).sum().item()) if want_pairs else None}
+    checks.update({"job_" + key: v for key, v in digests(pipe.counts, pipe.pairs if want_pairs else None,
+                                                       enc.n).items()})
+    stt = torch.tensor(list(A.draw_stats(enc).values()), dtype=torch.int64, device=dev)
+    if world > 1:
+        Dd._all_reduce(stt)
+    draw_stats = dict(zip(A.STAT_KEYS, (int(x) for x in stt.cpu().tolist())))
+    draw_stats["panels"] = Pj
+    result = {
+        "metric": "LEGACY panels/sec (node) at sf_e_110 shape; XtX MFMA util; speedup vs CPU",
+        "value": Pj / elapsed,
+        "unit": "panels/s",
+        "n_gpus": world,
+        "steps": steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / max(steps, 1) * 1e3,
+        "job_seconds": elapsed,
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "int32/u64 (integer draw), %s MFMA -> exact int pairs" % args.pair_engine,
+        "data": "synthetic instance %s (tests/golden/instances), Philox seed %d" % (inst_dir, args.seed),
+        "config": {"workload": "%s: ONE job of %d LEGACY panels over %d GPU(s) (shares of <= %d, chunks of %d), "
+                               "k=%d, n=%d, counts+%sunique over the whole job" % (
+                                   args.config, Pj, world, n_max, S, k, enc.n, "pairs+" if want_pairs else ""),
+                   "job_panels": Pj, "chunk_panels": S, "instance": inst_dir,
+                   "parallelism": "panel shards x%d" % world, "draw_kernel": draw_name,
+                   "pipeline": "every chunk's draw enqueued at once on the draw stream; counting follows per chunk"},
+        "checks": checks,
+        "draw_stats": draw_stats,
+        "cpu_baseline": None,
+    }
+    if rank == 0:
+        print(json.dumps(result))
+    if world > 1:
+        dist.destroy_process_group()
 
 
 def main():
@@ -313,6 +469,10 @@ def main():
     # --exchange bitmask
     xchg = Dd.PanelExchange(S, W, world, dev, redraw=(enc.handle, k, args.seed, 0) if args.exchange == "keys"
                             else None) if world > 1 else None
+
+    if args.job_panels:
+        return run_job(args, world, rank, dev, torch, dist, A, Dd, enc, k, S, inst_dir, pipe, want_pairs, stream,
+                       draw_name)
 
     overlap = not args.no_overlap
     nb = max(args.bufs, 2) if overlap else 1
@@ -436,6 +596,8 @@ def main():
     # single-GPU run with --panels N*P (same global panel indices)
     checks = {"last_step_unique": int(last["unique"].item()), "last_step_count_sum": int(pipe.counts.sum().item()),
               "last_step_pair_sum": int(torch.triu(pipe.pairs.view(enc.n, enc.n)).sum().item()) if want_pairs else None}
+    checks.update({"last_step_" + key: v for key, v in digests(pipe.counts, pipe.pairs if want_pairs else None,
+                                                                 enc.n).items()})
     # draw statistics of the timed steps, summed over ranks
     st = torch.tensor(list(A.draw_stats(enc).values()), dtype=torch.int64, device=dev)
     if world > 1:

@@ -77,6 +77,7 @@ SIGNATURES = {
                                           _I32, _P, _P, _P, _P, _P, _P, _P]),
     "csa_instance_set_address": (ctypes.c_int, [_P, _P]),
     "csa_instance_draw_stats": (ctypes.c_int, [_P, _I32, _P]),
+    "csa_instance_draw_stats_reset": (ctypes.c_int, [_P, _P]),
     "csa_exchange_keys_async": (ctypes.c_int, [_P, _P, _U64, _I32, _U64, _U32, _U64, _P, _U64, _P, _P, _P, _P]),
     "csa_unique_keys_scratch_bytes": (_U64, [_U64, _I32]),
     "csa_unique_keys_async": (ctypes.c_int, [_P, _I32, _U64, _U32, _P, _U32, _U64, _P, _P, _U64, _P, _P, _P]),

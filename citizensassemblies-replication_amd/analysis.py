@@ -153,8 +153,23 @@ class PanelSet:
         return self._count
 
     _where = "panels were not kept; only len() is available"
+    # a sharded run (distributed.ShardGather): the collective that brings the ranks' distinct panels
+    # to rank 0, made on first need; _root: this process is rank 0
+    _source = None
+    _root = True
+
+    def gather(self):
+        """Collective for a sharded run's found_panels (every rank calls it, or iterates / pickles):
+        the ranks' exact local distinct panels go to rank 0.  Called implicitly by iteration, `in`,
+        rows() and pickling; a no-op after the first time and for single-process results."""
+        if self._source is not None:
+            src, self._source = self._source, None
+            p = src()
+            if self._root:
+                self._packed = p
 
     def _materialise(self):
+        self.gather()
         if self._set is None:
             if self._packed is None:
                 raise RuntimeError(self._where)
@@ -179,7 +194,9 @@ class PanelSet:
 
     def rows(self):
         """The distinct panels as a host uint64[u, W] array (sorted rows), or None when the panels
-        were not kept.  Device panels are copied to the host here."""
+        were not kept (or on a rank other than 0 of a sharded run).  Device panels are copied to the
+        host here."""
+        self.gather()
         W = (self._n + 63) // 64
         if self._packed is None:
             if self._set is None:
@@ -271,6 +288,14 @@ STAT_KEYS = ("attempts", "selection_errors", "rejections")
 LAST_RUN_STATS = None
 
 
+def reset_draw_stats(enc, stream=None):
+    """Zero the instance's draw statistics before a batch: ordered on ``stream`` (a torch stream the
+    batch's draws run on; no host wait), or, without one, after the instance's own streams are idle
+    (csa_instance_draw_stats_reset) -- never a device-wide synchronisation."""
+    N.check(N.lib().csa_instance_draw_stats_reset(enc.handle, ctypes.c_void_p(stream.cuda_stream)
+                                                  if stream is not None else None))
+
+
 def draw_stats(enc, reset=False):
     """Totals of the instance's draws since creation / the last reset (csa_instance_draw_stats):
     {"attempts", "selection_errors", "rejections"}.  Synchronises the device."""
@@ -297,7 +322,7 @@ def legacy_sample_raw(enc, k, iterations, random_seed, panel_begin=0, want_pairs
         flags |= N.CSA_WANT_PANELS
     seed64 = int(random_seed) & 0xFFFFFFFFFFFFFFFF
     outs = (N.ptr(panels), N.ptr(counts), N.ptr(pairs), N.ptr(unique), N.ptr(attempts))
-    draw_stats(enc, reset=True)
+    reset_draw_stats(enc)
     if devices is None:
         rc = N.lib().csa_legacy_sample(enc.handle, int(k), seed64, panel_begin, S, flags, max_attempts, *outs)
     else:
@@ -339,7 +364,7 @@ def legacy_sample_device(enc, k, S, random_seed, keep_panels=True, chunk=1 << 20
         pairs = torch.empty(enc.n * enc.n, dtype=torch.int64, device=dev)
         pipe.reset(pairs=False)
         if host_panels is None:
-            draw_stats(enc, reset=True)
+            reset_draw_stats(enc, pipe.stream)
         own_p, own_h, own_pairs = pipe.panels, pipe.hashes, pipe.pairs
         pipe.pairs = pairs
         try:

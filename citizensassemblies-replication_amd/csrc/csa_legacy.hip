@@ -2018,13 +2018,15 @@ int launch_draw(const csa_instance *I, int32_t k, uint64_t seed, uint64_t panel_
     if (k == 0 && !single && !d_sel_out && !d_present_out) {
         int rejected = 0;
         for (int f = 0; f < I->F; ++f) rejected |= I->sel0[f] < I->fmin[f];
+        // draw statistics as the kernels keep them: accepted new panels only (an index-list re-draw of
+        // the multi-GPU owner passes its list capacity as n_panels and draws no new panel)
+        if (!rejected && !d_panel_list) const_cast<csa_instance *>(I)->panels_drawn += n_panels;
         if (!d_panels) {  // pick-list draw of k = 0: nothing to write but the attempts / status
             hipLaunchKernelGGL(empty_panels_kernel, dim3((unsigned)((n_panels + 255) / 256)), dim3(256), 0, stream,
                                n_panels, d_attempts, d_status, panel_begin, rejected);
             HIPCHK(hipGetLastError());
             return CSA_OK;
         }
-        if (!rejected) const_cast<csa_instance *>(I)->panels_drawn += n_panels;
         HIPCHK(hipMemsetAsync(d_panels, 0, n_panels * I->W * 8, stream));
         hipLaunchKernelGGL(empty_panels_kernel, dim3((unsigned)((n_panels + 255) / 256)), dim3(256), 0, stream,
                            n_panels, d_attempts, d_status, panel_begin, rejected);
@@ -2381,6 +2383,27 @@ int csa_instance_draw_stats(csa_instance *I, int32_t reset, uint64_t *out) {
         }
     }
     for (int j = 0; j < 3; ++j) out[j] = acc[j];
+    return CSA_OK;
+}
+
+int csa_instance_draw_stats_reset(csa_instance *I, void *stream) {
+    if (!I) return fail(CSA_E_INVALID, "draw_stats_reset: null instance");
+    std::vector<csa_instance *> all{I};
+    for (csa_instance *R : I->replicas)
+        if (R) all.push_back(R);
+    for (csa_instance *X : all) {
+        ScopedDevice sd(X->device);
+        if (stream && X == I) {  // ordered on the caller's stream: no host wait
+            HIPCHK(hipMemsetAsync(X->d_stats, 0, 16, (hipStream_t)stream));
+        } else {  // only the instance's own streams (csa_legacy_sample's pipeline), not the device
+            for (hipStream_t s : {X->sdraw, X->spost, X->stream})
+                if (s) HIPCHK(hipStreamSynchronize(s));
+            if (!X->stream) HIPCHK(hipStreamCreateWithFlags(&X->stream, hipStreamNonBlocking));
+            HIPCHK(hipMemsetAsync(X->d_stats, 0, 16, X->stream));
+            HIPCHK(hipStreamSynchronize(X->stream));
+        }
+        X->panels_drawn = 0;
+    }
     return CSA_OK;
 }
 

@@ -398,42 +398,77 @@ def local_distinct_rows(hashes, panels, n, W, status=None, stream=None):
     return send_p[: cnt * W], cnt
 
 
-def gather_distinct_to_root(hashes, panels, n, W, status=None, stream=None):
-    """found_panels of a sharded run, on rank 0 only: every rank reduces its shard to its exact local
-    distinct panels, and rank 0 receives them one rank at a time (a buffer sized for that rank, copied
-    to the host before the next), so no rank ever holds the whole job's panels on its device.
-    Returns uint64[m, W] on rank 0 (rows of all ranks; a panel drawn on two ranks appears twice and
-    PanelSet deduplicates on iteration), None elsewhere."""
+GATHER_CHUNK_BYTES = 256 << 20   # rows per point-to-point message of the found_panels gather
+
+
+def gather_distinct_to_root(hashes, panels, n, W, status=None, stream=None, chunk_bytes=None):
+    """found_panels of a sharded run, on rank 0 only (a collective: every rank calls it): every rank
+    reduces its shard to its exact local distinct panels; one all_reduce tells rank 0 every rank's
+    count, rank 0 allocates ONE host array for all of them and receives each rank's rows straight
+    into its slice, in messages of at most ``chunk_bytes`` (no concatenated copy; over RCCL each
+    message lands in a device buffer of that size first), so no rank ever holds more than its own
+    panels on its device.  Returns uint64[m, W] on rank 0 (rows of all ranks; a panel drawn on two
+    ranks appears twice and PanelSet deduplicates on iteration), None elsewhere."""
     import torch
     import torch.distributed as dist
     world, r = dist.get_world_size(), dist.get_rank()
+    W = int(W)
     rows, cnt = local_distinct_rows(hashes, panels, n, W, status, stream)
     host = _host_collectives(rows) or not rows.is_cuda
     dev = torch.device("cpu") if host else rows.device
+    counts = torch.zeros(world, dtype=torch.int64, device=dev)
+    counts[r] = cnt
+    _all_reduce(counts)
+    counts = [int(c) for c in counts.cpu().tolist()]
+    per = max(1, int(chunk_bytes or GATHER_CHUNK_BYTES) // (8 * max(W, 1)))   # rows per message
     if r != 0:
-        dist.send(torch.tensor([cnt], dtype=torch.int64, device=dev), 0)
-        if cnt:
-            dist.send(rows.cpu() if host else rows.contiguous(), 0)
+        src = rows.cpu() if host else rows.contiguous()
+        for o in range(0, cnt, per):
+            dist.send(src[o * W:min(cnt, o + per) * W], 0)
         return None
-    parts = [rows.cpu().numpy().view(np.uint64).reshape(cnt, W)]
-    for src in range(1, world):
-        c = torch.zeros(1, dtype=torch.int64, device=dev)
-        dist.recv(c, src)
-        c = int(c.item())
-        if c:
-            buf = torch.empty(c * W, dtype=torch.int64, device=dev)
-            dist.recv(buf, src)
-            parts.append(buf.cpu().numpy().view(np.uint64).reshape(c, W))
-            del buf
-    return np.concatenate(parts)
+    out = np.empty((sum(counts), W), np.uint64)
+    out[:cnt] = rows.cpu().numpy().view(np.uint64).reshape(cnt, W)
+    del rows
+    buf = None if host else torch.empty(min(per, max(counts)) * W, dtype=torch.int64, device=dev)
+    at = cnt
+    for src_rank in range(1, world):
+        c = counts[src_rank]
+        for o in range(0, c, per):
+            m = min(per, c - o)
+            dst = torch.from_numpy(out[at + o:at + o + m].reshape(-1).view(np.int64))
+            if host:
+                dist.recv(dst, src_rank)                # gloo: straight into the host array
+            else:
+                dist.recv(buf[: m * W], src_rank)
+                dst.copy_(buf[: m * W])
+        at += c
+    return out
+
+
+class ShardGather:
+    """found_panels of a sharded run before anyone looked at them: this rank's shard (hashes and
+    panels, kept on its device) and how to gather the ranks' exact local distinct panels to rank 0.
+    Calling it is the collective gather_distinct_to_root (every rank must call it, once); until then
+    legacy_probabilities has sent nothing -- len(found_panels) is the global exact count from the
+    exchange."""
+
+    def __init__(self, hashes, panels, n, W, stream=None):
+        self.hashes, self.panels, self.n, self.W, self.stream = hashes, panels, int(n), int(W), stream
+
+    def __call__(self):
+        out = gather_distinct_to_root(self.hashes, self.panels, self.n, self.W, stream=self.stream)
+        self.hashes = self.panels = None
+        return out
 
 
 def legacy_probabilities_distributed(instance, iterations, random_seed, keep_panels=True):
     """analysis.py:162-191 with the panels sharded over the ranks of the default group.  Every rank
     returns the whole job's alloc, pair histogram and exact distinct-panel count.  With
-    ``keep_panels`` rank 0's ``found_panels`` also iterates like the reference's set (the ranks'
-    exact local distinct panels are sent to rank 0, one rank at a time); on the other ranks it
-    supports len() only.  The draw statistics (analysis.LAST_RUN_STATS) are summed over ranks."""
+    ``keep_panels`` rank 0's ``found_panels`` also iterates like the reference's set: each rank keeps
+    its shard on its device, and the first iteration / `in` / rows() / pickle of found_panels -- a
+    collective, made on every rank (PanelSet.gather) -- sends the ranks' exact local distinct panels
+    to rank 0; on the other ranks it supports len() only.  The draw statistics
+    (analysis.LAST_RUN_STATS) are summed over ranks."""
     import torch
     from . import analysis as A
     from .device import DevicePipeline
@@ -450,7 +485,7 @@ def legacy_probabilities_distributed(instance, iterations, random_seed, keep_pan
     torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", r)) % max(torch.cuda.device_count(), 1))
     pipe = DevicePipeline(enc, instance.k, max(local, 1), want_pairs=True, want_unique=True)
     pipe.reset()
-    A.draw_stats(enc, reset=True)
+    A.reset_draw_stats(enc, pipe.stream)
     if local:
         pipe.draw(random_seed, begin, local)
         pipe.transpose_count(local)
@@ -462,11 +497,14 @@ def legacy_probabilities_distributed(instance, iterations, random_seed, keep_pan
     _raise_together(pipe.status, pipe.stream)
     stats = torch.tensor(list(A.draw_stats(enc).values()), dtype=torch.int64, device=pipe.counts.device)
     _all_reduce(stats)
-    panels = gather_distinct_to_root(pipe.hashes[: 2 * local], pipe.panels[: local * enc.W], local, enc.W,
-                                     pipe.status, pipe.stream) if keep_panels else None
-    raw = A.LegacyRaw(counts.cpu().numpy(), pairs.cpu().numpy().reshape(enc.n, enc.n), int(u.item()), panels, None,
+    raw = A.LegacyRaw(counts.cpu().numpy(), pairs.cpu().numpy().reshape(enc.n, enc.n), int(u.item()), None, None,
                       dict(zip(A.STAT_KEYS, (int(x) for x in stats.cpu().tolist()))))
     out = A.finish(instance, enc, raw, S)
-    if keep_panels and r != 0:
+    if keep_panels:
+        # lazy: the shard stays on this rank's device; the first iteration / `in` / rows() / pickle of
+        # found_panels (a collective -- every rank makes it) gathers the distinct panels to rank 0
+        out[1]._source = ShardGather(pipe.hashes[: 2 * local], pipe.panels[: local * enc.W], local, enc.W,
+                                     pipe.stream)
+        out[1]._root = r == 0
         out[1]._where = "found_panels of a sharded run iterate on rank 0 only (len() is global)"
     return out

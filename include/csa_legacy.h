@@ -85,6 +85,11 @@ int csa_instance_set_state(csa_instance *inst, const int32_t *sel, const int32_t
  *   out[2] min-quota rejections (check_min_cats false after k picks, legacy.py:160-168)
  * Synchronises the instance's device(s); reset != 0 zeroes the totals after reading them. */
 int csa_instance_draw_stats(csa_instance *inst, int32_t reset, uint64_t *out);
+/* Zero the draw statistics without a device-wide synchronisation: with a stream, a memset
+ * ordered on it (draws the caller enqueues after it on that stream count from zero); with NULL,
+ * after the instance's own streams (csa_legacy_sample's pipeline) are idle.  Other streams of the
+ * device are never waited for. */
+int csa_instance_draw_stats_reset(csa_instance *inst, void *stream);
 
 /* check_same_address (legacy.py:78-99, 103-113): addr_next (n int32) links the agents that share
  * an address (the check_same_address_columns values) into rings, agent order: addr_next[p] = the

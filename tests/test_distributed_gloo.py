@@ -56,14 +56,38 @@ def _worker(rank, world, port, out_dir, name):
     pairs = torch.from_numpy(coracle.pairs(panels, o.n, threads=2).ravel().copy())
     hashes = torch.from_numpy(D.panel_hashes(panels).ravel().view(np.int64).copy())
     ptens = torch.from_numpy(np.ascontiguousarray(panels).view(np.int64).ravel().copy())
+    recvs = []
+    real_recv = dist.recv
+
+    def counting_recv(tensor, src=None, *a, **kw):   # every point-to-point receive of this rank
+        recvs.append(tensor.numel())
+        return real_recv(tensor, src, *a, **kw)
+
+    dist.recv = counting_recv
     counts, pairs, u = D.combine(counts, pairs, hashes, ptens, W)
-    rows = D.gather_distinct_to_root(hashes, ptens, e - b, W)     # found_panels: rank 0 only
-    assert (rows is None) == (rank != 0)
+    # found_panels as legacy_probabilities_distributed returns it: nothing gathered yet, len() global
+    A = pkg("analysis")
+    found = A.PanelSet(int(u.item()), None, o.n, list(range(o.n)))
+    found._source, found._root = D.ShardGather(hashes, ptens, e - b, W), rank == 0
+    assert len(found) == int(u.item()) and recvs == []
+    D.GATHER_CHUNK_BYTES = 8 * W * 7               # 7 rows per message: several messages per rank
     if rank == 0:
+        tuples = sorted(found)                     # the collective gather, then the set
+        rows = found.rows()
+        import pickle
+        again = pickle.loads(pickle.dumps(found))
+        assert sorted(again) == tuples and len(again) == len(found)
+        assert all(t in found for t in tuples[:5]) and (-1,) not in found
+        np.save(os.path.join(out_dir, "recvs.npy"), np.array(recvs, np.int64))
         np.save(os.path.join(out_dir, "rows.npy"), rows)
         np.save(os.path.join(out_dir, "counts.npy"), counts.numpy())
         np.save(os.path.join(out_dir, "pairs.npy"), pairs.numpy())
         np.save(os.path.join(out_dir, "unique.npy"), np.array([int(u.item())]))
+    else:
+        found.gather()                             # this rank's side of the collective
+        with pytest.raises(RuntimeError):
+            iter(found)
+        assert recvs == []
     dist.barrier()
     dist.destroy_process_group()
 
@@ -86,10 +110,12 @@ def test_gloo_exchange_matches_single_run(tmp_path, world, name):
         # duplicates really are split across ranks: every shard holds most of the 100 panels
         assert want == 100
     assert int(np.load(tmp_path / "unique.npy")[0]) == want
-    # the rows gathered on rank 0 (each rank's local distinct set) cover exactly the distinct panels
+    # the rows gathered on rank 0 (each rank's local distinct set) are exactly the distinct panels
+    # (PanelSet.rows deduplicates), received in messages of <= 7 rows, none before iteration
     rows = np.load(tmp_path / "rows.npy")
-    assert len(rows) <= min(S, world * want)
-    assert np.array_equal(np.unique(rows, axis=0), np.unique(panels, axis=0))
+    assert np.array_equal(rows, np.unique(panels, axis=0))
+    recvs = np.load(tmp_path / "recvs.npy")
+    assert len(recvs) >= world - 1 and recvs.max() <= 7 * panels.shape[1]
 
 
 def _collision_worker(rank, world, port, out_dir):
@@ -201,3 +227,29 @@ def test_bench_self_launch_world2(tmp_path, capfd):
     got = json.loads(line[0])
     assert got == {"world": 2, "sum": 3, "argv": ["--gpus", "2", "--steps", "1"], "local": "0",
                    "addr": "127.0.0.1"}
+
+
+_FAILING_RANK_SCRIPT = r"""
+import os, sys, time
+import torch.distributed as dist
+if os.environ["RANK"] == "1":
+    sys.exit(3)                 # this rank dies before the rendezvous
+dist.init_process_group("gloo")  # rank 0 would wait here for rank 1 until the store's timeout
+"""
+
+
+def test_bench_self_launch_fails_fast(tmp_path):
+    """self_launch with one rank exiting non-zero at startup: the other rank (blocked in the
+    rendezvous) is terminated and the failing rank's exit code returned within seconds, not after the
+    rendezvous timeout."""
+    import importlib.util
+    import time
+    spec = importlib.util.spec_from_file_location("bench", os.path.join(REPO, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    script = tmp_path / "rank.py"
+    script.write_text(_FAILING_RANK_SCRIPT)
+    t = time.time()
+    rc = bench.self_launch(2, script=str(script), argv=[], grace=5.0)
+    assert rc == 3
+    assert time.time() - t < 60

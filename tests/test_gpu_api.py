@@ -149,6 +149,28 @@ def test_draw_stats_match_reference(gpu_available, case):
     assert A.LAST_RUN_STATS == raw.stats
 
 
+def test_draw_stats_k0(gpu_available):
+    """k = 0 takes the host fast path (empty panels, no kernel draw): every panel is one accepted
+    attempt when no min is positive, in the bitmask form and in the pick-list form alike (ADVICE r03:
+    the pick-list form counted nothing).  That re-draws of the multi-GPU owner add no panels is
+    checked by test_bench_job_mode_two_ranks_equals_one (couples: equal draw statistics at N = 2)."""
+    import torch
+    N = pkg("_native")
+    A = pkg("analysis")
+    inst = _inst("couples_panel_from_twenty_people_no_constraints_2", 0)
+    enc = pkg().encode(inst.categories, inst.agents)
+    raw = A.legacy_sample_raw(enc, 0, 1000, 3, want_pairs=False, want_panels=False)
+    assert raw.stats == {"attempts": 1000, "selection_errors": 0, "rejections": 0}
+    assert raw.unique == 1
+    A.draw_stats(enc, reset=True)
+    st = torch.zeros(4, dtype=torch.int32, device="cuda")
+    picks = torch.empty(8, dtype=torch.int16, device="cuda")
+    N.check(N.lib().csa_draw_picks_async(enc.handle, 0, 3, 0, 500, 0, N.ptr(picks), None, N.ptr(st), None))
+    torch.cuda.synchronize()
+    assert int(st[0].item()) == 0
+    assert A.draw_stats(enc) == {"attempts": 500, "selection_errors": 0, "rejections": 0}
+
+
 def test_exchange_local_distinct_beyond_partitioned_path(gpu_available):
     """csa_exchange_pack_async on 8192 x 2048 + 4096 entries (the partitioned dedupe's limit + 1
     block): the global-table fallback lists exactly one index per distinct panel."""
@@ -191,8 +213,28 @@ def test_bench_self_launch_two_ranks_equals_one(gpu_available):
     two = _bench(["--gpus", "2", "--panels", "20000"] + common, {"CSA_BENCH_BACKEND": "gloo"})
     one = _bench(["--gpus", "1", "--panels", "40000"] + common, {})
     assert two["n_gpus"] == 2 and one["n_gpus"] == 1
-    for key in ("last_step_unique", "last_step_count_sum", "last_step_pair_sum"):
+    for key in ("last_step_unique", "last_step_count_sum", "last_step_pair_sum", "last_step_counts_sha256",
+                "last_step_pairs_triu_sha256"):
         assert two["checks"][key] == one["checks"][key]
     assert two["checks"]["sample_devices"]["equal_to_rank_sharded"] is True
     st = two["draw_stats"]
     assert st["attempts"] == st["panels"] + st["selection_errors"] + st["rejections"]
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("config,panels,chunk", [("sf_e_110", 90001, 20000), ("synthetic8192", 30001, 8000),
+                                                 ("couples", 100001, 30000)])
+def test_bench_job_mode_two_ranks_equals_one(gpu_available, config, panels, chunk):
+    """bench.py --job-panels P (strong scaling: ONE job of P panels split over the ranks, accumulated
+    counts / pairs, the exact distinct count over the whole job): the 2-rank gloo rehearsal on this GPU
+    and the 1-GPU run agree on the count vector and the pair triangle (SHA-256 digests), the distinct
+    count and the draw statistics; uneven shares (P odd) and a ragged last chunk included."""
+    common = ["--config", config, "--job-panels", str(panels), "--panels", str(chunk), "--warmup", "1",
+              "--no-cpu-baseline", "--no-api"]
+    two = _bench(["--gpus", "2"] + common, {"CSA_BENCH_BACKEND": "gloo"})
+    one = _bench(["--gpus", "1"] + common, {})
+    assert two["scaling"] == one["scaling"] == "strong"
+    for key in ("job_unique", "job_count_sum", "job_pair_sum", "job_counts_sha256", "job_pairs_triu_sha256"):
+        assert two["checks"][key] == one["checks"][key], key
+    assert two["draw_stats"] == one["draw_stats"]
+    assert one["steps"] == (panels + chunk - 1) // chunk

@@ -505,16 +505,33 @@ def _dist_worker(rank, world, port, out_dir, name, k, S, seed):
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
+        import pickle
         A = pkg("analysis")
         inst = pkg().read_instance(*inst_paths(name), k)
+        recvs = []
+        real_recv = dist.recv
+
+        def counting_recv(tensor, src=None, *a, **kw):
+            recvs.append(int(tensor.numel()))
+            return real_recv(tensor, src, *a, **kw)
+
+        dist.recv = counting_recv
         alloc, found, hist = A.legacy_probabilities(inst, S, seed)      # world > 1: sharded
+        assert recvs == []      # found_panels are gathered lazily, not by legacy_probabilities
         if rank == world - 1:
             np.save(os.path.join(out_dir, "unique_last.npy"), np.array([len(found)]))
         if rank == 0:           # found_panels iterate on rank 0 (the ranks' distinct panels gathered)
             np.save(os.path.join(out_dir, "alloc.npy"), np.array([alloc[i] for i in range(len(alloc))]))
             np.save(os.path.join(out_dir, "upper.npy"), hist.upper())
             np.save(os.path.join(out_dir, "unique.npy"), np.array([len(found)]))
-            np.save(os.path.join(out_dir, "found.npy"), np.array(sorted(found)))
+            tuples = sorted(found)                                     # the collective gather
+            assert recvs
+            assert all(t in found for t in tuples[:3])
+            np.save(os.path.join(out_dir, "found.npy"), np.array(tuples))
+            with open(os.path.join(out_dir, "result.pkl"), "wb") as f:
+                pickle.dump((alloc, found, hist), f)
+        else:
+            pickle.dumps((alloc, found, hist))  # pickling is the other ranks' side of the gather
         dist.barrier()
     finally:
         dist.destroy_process_group()
@@ -525,7 +542,8 @@ def _dist_worker(rank, world, port, out_dir, name, k, S, seed):
 def test_legacy_probabilities_distributed_gloo(gpu_available, tmp_path, name, k, S, seed):
     """analysis.legacy_probabilities with a 2-rank process group (both ranks on this GPU, gloo:
     RCCL refuses two ranks on one device): the sharded draw, the exact panel exchange and the
-    gathered found_panels equal the single-GPU result."""
+    found_panels -- gathered to rank 0 only when iterated / pickled (no dist.recv before), `in`,
+    and the pickled tuple -- equal the single-GPU result."""
     import socket
     import torch.multiprocessing as mp
     A = pkg("analysis")
@@ -540,6 +558,10 @@ def test_legacy_probabilities_distributed_gloo(gpu_available, tmp_path, name, k,
     assert int(np.load(tmp_path / "unique.npy")[0]) == len(found)
     assert int(np.load(tmp_path / "unique_last.npy")[0]) == len(found)
     assert np.load(tmp_path / "found.npy").tolist() == [list(p) for p in sorted(found)]
+    import pickle
+    with open(tmp_path / "result.pkl", "rb") as f:
+        _, found_p, _ = pickle.load(f)
+    assert sorted(found_p) == sorted(found) and len(found_p) == len(found)
 
 
 def test_n16384_boundary(gpu_available):
