@@ -2505,13 +2505,15 @@ int csa_pairs_unpack_async(const int32_t *d_packed, int32_t n, int64_t *d_pairs,
 }
 
 #ifdef CSA_LANE_STAMPS
-// diagnostic builds only: the draw_lane_kernel segment totals (cycles summed over waves, [8] = waves)
-int csa_debug_lane_stamps(uint64_t *out16, int reset) {
+// diagnostic builds only: the draw_lane_kernel segment totals (cycles summed over waves, [8] = waves,
+// [9..19] = region execution counts summed over waves: loop, philox, step, pick, store, round, pass2,
+// pass1, nocand, kcheck, ending)
+int csa_debug_lane_stamps(uint64_t *out24, int reset) {
     HIPCHK(hipDeviceSynchronize());
-    HIPCHK(hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_lane_stamps), 16 * 8));
+    HIPCHK(hipMemcpyFromSymbol(out24, HIP_SYMBOL(g_lane_stamps), 24 * 8));
     if (reset) {
-        static const unsigned long long zero[16] = {};
-        HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_lane_stamps), zero, 16 * 8));
+        static const unsigned long long zero[24] = {};
+        HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_lane_stamps), zero, 24 * 8));
     }
     return CSA_OK;
 }

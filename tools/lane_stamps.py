@@ -38,7 +38,7 @@ def main():
     fn = L.csa_debug_lane_stamps
     fn.restype = ctypes.c_int
     fn.argtypes = [ctypes.c_void_p, ctypes.c_int]
-    out = (ctypes.c_uint64 * 16)()
+    out = (ctypes.c_uint64 * 24)()
     S = args.panels
     pipe = Dv.DevicePipeline(enc, k, S, want_pairs=False, want_unique=False)
     pipe.reset()
@@ -54,12 +54,17 @@ def main():
     pipe.check_status()
     N.check(fn(out, 1))
     names = ["attempt starts + Philox", "step (argmax, scan, select, decrements)", "cascades", "bookkeeping + loop"]
-    tot = sum(out[q] for q in range(4))
+    tot = max(1, sum(out[q] for q in range(4)))
     waves = out[8]
     res = {"config": args.config, "panels": S, "kernel": pipe.draw_kernel_name(), "ms": ev[0].elapsed_time(ev[1]),
            "waves": waves, "cycles_per_wave": tot / max(waves, 1),
            "share": {names[q]: out[q] / tot for q in range(4)},
-           "cycles_per_wave_by_segment": {names[q]: out[q] / max(waves, 1) for q in range(4)}}
+           "cycles_per_wave_by_segment": {names[q]: out[q] / max(waves, 1) for q in range(4)},
+           # region execution counts per wave (tools/valu_budget.py multiplies them with the regions'
+           # static VALU classes)
+           "region_runs_per_wave": {r: out[9 + q] / max(waves, 1) for q, r in enumerate(
+               ("loop", "philox", "step", "pick", "store", "round", "pass2", "pass1", "nocand", "kcheck",
+                "ending"))}}
     print(json.dumps(res, indent=1))
 
 
