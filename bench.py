@@ -210,24 +210,17 @@ def cpu_baseline(inst_dir, k, seed, target_s, want_pairs):
     return out
 
 
-def load_valu_peak():
-    """Integer VALU issue roof of one MI355X (wave-instructions/s over the chip): tools/valu_rate.hip
-    on the GPU box, 8 waves/SIMD of independent v_add_u32 / v_bcnt / v_cndmask / v_mul_i32_i24_sdwa
-    chains (profiles/valu_rate_mi355x.jsonl): the ~4.2-cycle class of wave64 instructions (an SGPR
-    operand, bcnt, cndmask, mul24, shifts left, 3-source ops, DPP).  Two-operand add/and/or/xor/mov with
-    VGPR or constant operands issue every ~2.3 cycles in a homogeneous stream but not in the draw
-    kernels' mixed ones (profiles/valu_enc_mi355x.jsonl), so this is the roof."""
-    path = os.path.join(REPO, "profiles", "valu_rate_mi355x.jsonl")
+def load_valu_budget(config):
+    """Class-weighted VALU budget of the draw kernel (tools/valu_budget.py, profiles/valu_budget_<config>.json):
+    its dynamic VALU mix split into the two issue classes measured by tools/coissue.hip -- two-operand
+    add/and/or/xor/mov/lshr with VGPR or constant operands, which two waves of a SIMD issue together
+    (2.47 SIMD cycles each), and everything else (bcnt, cndmask, mul24, 3-source ops, DPP, SDWA, an SGPR
+    operand: one per ~4.3 cycles) -- priced per panel.  That budget is the kernel's VALU roof."""
+    path = os.path.join(REPO, "profiles", "valu_budget_%s.json" % config)
     if not os.path.exists(path):
         return None
     with open(path) as fh:
-        rows = [json.loads(line) for line in fh if line.strip()]
-    # the saturated rate: the most waves per SIMD the microbenchmark ran (8; 1, 2, 4 show the ramp)
-    top = max(r.get("waves_per_simd", 8) for r in rows)
-    rows = [r for r in rows if r.get("waves_per_simd", 8) == top]
-    ints = [r["wave_inst_per_s_chip"] for r in rows if r["op"] in ("v_add_u32", "v_bcnt", "v_cndmask", "v_mul24_sdwa")]
-    return {"peak_wave_inst_per_s": sum(ints) / len(ints), "source": "profiles/valu_rate_mi355x.jsonl",
-            "waves_per_simd": top, "ops": {r["op"]: r["wave_inst_per_s_chip"] for r in rows}} if ints else None
+        return json.load(fh)
 
 
 def load_pmc(config):
@@ -723,24 +716,32 @@ def main():
                             "algorithmic output bytes (%s) over its in-region time (the HBM "
                             "framing the contract asks for); roofline.valu is the binding roof: its VALU "
                             "wave-instructions per second (rocprofv3 SQ_INSTS_VALU of these sources) over the "
-                            "integer VALU issue rate measured on the chip (tools/valu_rate.hip); issue_frac_2cyc "
-                            "is the same count priced at 2 cycles per wave-instruction, which integer VALU does "
-                            "not reach") % ("2k B of pick list per panel" if split else
+                            "rate the kernel's class mix allows (tools/valu_budget.py: single-issue VALU 4.3, "
+                            "dual-issue 2.47 SIMD cycles per wave-instruction, tools/coissue.hip); issue_frac_2cyc "
+                            "is the same count priced at 2 cycles per wave-instruction") % ("2k B of pick list per panel" if split else
                                              "8W + 16 B of packed panel and hash per panel")
             if pmc_ok and pmc.get("draw_issue") and pmc.get("draw_kernel") == draw_name:
                 kernels["draw"]["pmc_issue"] = pmc["draw_issue"]
                 roof["issue_frac_2cyc"] = pmc["draw_issue"].get("valu_issue_frac")
                 roof["mean_waves_per_simd"] = pmc["draw_issue"].get("mean_waves_per_simd")
-                # the roof that binds: VALU instructions of this kernel (PMC, same sources) per second
-                # in the timed region vs the measured integer VALU issue rate of the chip
-                vp = load_valu_peak()
-                if vp and stage_pipe["draw"] > 0:
-                    rate = pmc["draw_issue"]["valu_insts_per_panel"] * S / (stage_pipe["draw"] * 1e-3)
-                    roof["valu"] = {"bound": "valu_issue", "achieved": rate, "peak": vp["peak_wave_inst_per_s"],
-                                    "unit": "wave-instructions/s", "frac": rate / vp["peak_wave_inst_per_s"],
-                                    "valu_insts_per_panel": pmc["draw_issue"]["valu_insts_per_panel"],
+                # the roof that binds: VALU instructions of this kernel (PMC, same sources) per second in
+                # the timed region vs the rate its class mix allows at the clock it runs at (every
+                # single-issue instruction 4.3 cycles of its SIMD, every dual-issue one 2.47 cycles);
+                # single_issue: one VALU per 4 cycles per SIMD (the quad rate, SQ_ACTIVE_INST_VALU)
+                vb = load_valu_budget(args.config)
+                if vb and stage_pipe["draw"] > 0:
+                    vpp = pmc["draw_issue"]["valu_insts_per_panel"]
+                    clk = pmc["draw_issue"]["clock_GHz"] * 1e9
+                    rate = vpp * S / (stage_pipe["draw"] * 1e-3)
+                    peak = vpp / vb["budget_class_weighted_cycles_per_panel"] * 1024 * clk
+                    roof["valu"] = {"bound": "valu_issue", "achieved": rate, "peak": peak,
+                                    "unit": "wave-instructions/s", "frac": rate / peak,
+                                    "single_issue_peak": 1024 * clk / 4, "single_issue_frac": rate / (1024 * clk / 4),
+                                    "valu_insts_per_panel": vpp, "half_rate_frac": vb["valu_per_panel"]["half_frac"],
+                                    "clock_GHz": clk / 1e9,
                                     "pmc_valu_active_frac": pmc["draw_issue"].get("valu_active_frac"),
-                                    "peak_source": vp["source"]}
+                                    "peak_source": "profiles/valu_budget_%s.json (tools/valu_budget.py: class-weighted "
+                                                   "budget of the kernel's dynamic VALU mix)" % args.config}
     roof["pmc_source_sha"] = sha
     roof["pmc_matches_sources"] = pmc_ok
 

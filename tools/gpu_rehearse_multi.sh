@@ -17,11 +17,12 @@ CSA_BENCH_BACKEND=gloo timeout -k 10 300 python bench.py --config $CFG --gpus 2 
 rc=$?; echo "[n2 self-launch] rc=$rc"; [ $rc -eq 0 ] || { tail -20 "$OUT/reh_n2s.err"; exit $rc; }
 python3 - "$OUT/reh_n1.json" "$OUT/reh_n2.json" "$OUT/reh_n2s.json" <<'PY'
 import json, sys
-KEYS = ("last_step_unique", "last_step_count_sum", "last_step_pair_sum")
-a = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
+KEYS = ("last_step_unique", "last_step_count_sum", "last_step_pair_sum", "last_step_counts_sha256",
+        "last_step_pairs_triu_sha256")
+a = json.loads([ln for ln in open(sys.argv[1]) if ln.startswith("{")][-1])
 print("n1", a["n_gpus"], {k: a["checks"][k] for k in KEYS}, "value %.1fM" % (a["value"] / 1e6))
 for f in sys.argv[2:]:
-    b = json.loads(open(f).read().strip().splitlines()[-1])
+    b = json.loads([ln for ln in open(f) if ln.startswith("{")][-1])
     print("n2", b["n_gpus"], {k: b["checks"][k] for k in KEYS}, "value %.1fM" % (b["value"] / 1e6), "exchange",
           b["kernels"].get("exchange"), "draw stream busy %.3f" % b["draw_stream_busy"], "draw_stats", b["draw_stats"],
           "sample_devices", b["checks"].get("sample_devices"))
