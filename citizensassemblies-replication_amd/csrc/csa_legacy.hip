@@ -2758,7 +2758,10 @@ int csa_draw_kernel_name(const csa_instance *I, int32_t k, char *buf, uint64_t l
 
 int32_t csa_xt_pad(int32_t n) { return ((n + kPairBlock - 1) / kPairBlock) * kPairBlock; }
 
-constexpr bool kXtWaveDefault = false;  // xt_wave_kernel unless CSA_XT_KERNEL says otherwise
+// xt_wave_kernel by default for narrow panels only (tools/xt_bench.py, 10^6 panels: W = 4 0.039 vs 0.054 ms;
+// W = 27 0.109 vs 0.113; W = 32 0.126 vs 0.120; W = 128 0.418 vs 0.395 -- the barrier-per-block kernel
+// keeps more loads in flight per CU once a block is wide)
+inline bool xt_wave_default(int W) { return W <= 8; }
 
 int csa_transpose_count_async(const uint64_t *d_panels, uint64_t n_panels, int32_t n, uint64_t *d_xt,
                               int64_t *d_counts, void *stream) {
@@ -2779,7 +2782,7 @@ int csa_transpose_count_async(const uint64_t *d_panels, uint64_t n_panels, int32
             cus = 256;
     }
     const char *xk = getenv("CSA_XT_KERNEL");  // "wave" | "lds" (the barrier-per-block xt_count_kernel)
-    if (xk ? !strcmp(xk, "wave") : kXtWaveDefault) {
+    if (xk ? !strcmp(xk, "wave") : xt_wave_default(W)) {
         // xt_wave_kernel: one pass of workgroups (two per CU: 4 tiles of <= 17 KB each), blocks
         // per workgroup a multiple of the wave count
         const uint64_t per = std::max<uint64_t>(1, (nblk * ranges + 2 * (uint64_t)cus - 1) / (2 * (uint64_t)cus));
