@@ -576,7 +576,6 @@ __global__ __launch_bounds__(draw_threads(FPL, WPL), draw_occupancy(FPL, WPL)) v
 }
 
 #include "draw_lane.inc"
-#include "draw_lanel.inc"
 #include "draw_wide.inc"
 #include "draw_solo.inc"
 
@@ -1907,7 +1906,6 @@ int check_k(const csa_instance *I, int32_t k) {
 struct DrawConfig {
     int G = 16, FPL = 1, WPL = 1;
     bool lane = false;  // draw_lane_kernel (2 lanes per panel): FPL / WPL hold its FN / WN
-    bool lanel = false; // (with lane) draw_lanel_kernel: the same layout, the pool in LDS
     bool wide = false;  // draw_wide_kernel (8 lanes per panel)
     bool solo = false;  // draw_solo_kernel (1 lane per panel): FPL / WPL hold its FN / WN
     const void *fn = nullptr;
@@ -1977,15 +1975,6 @@ const void *solo_fn(int fn_, int wn) {
     }
 }
 
-const void *lanel_fn(int fn_, int wn) {
-    if (fn_ != 32) return nullptr;
-    switch (wn) {
-        case 16: return reinterpret_cast<const void *>(&draw_lanel_kernel<32, 16>);
-        case 28: return reinterpret_cast<const void *>(&draw_lanel_kernel<32, 28>);
-        default: return nullptr;
-    }
-}
-
 const void *lane_fn(int fn_, int wn) {
     switch (fn_) {
         case 32: return lane_fn_w<32>(wn);
@@ -2032,8 +2021,6 @@ int pow2_ceil_int(int x) {
 // need <= min - max) -- else draw_kernel with G = 16 (F <= 64, W <= 256) or 64.  Pick-order /
 // single-attempt draws (general mode) use draw_kernel<64, ..., true>.  CSA_DRAW_KERNEL=solo|lane|wide|16|64
 // forces a batch kernel the instance fits (parity tests of every layout).
-constexpr bool kLanelDefault = false;  // draw_lanel_kernel by default for the shapes it is built for
-
 int pick_draw_config(const csa_instance *I, bool general, DrawConfig &c) {
     general = general || I->d_addr_next;  // same-address deletions: draw_kernel<64, ..., true> only
     const bool lane_ok = I->F <= 32 && I->d_pmask && !I->zero_max_min && I->W <= 32 && I->max_abs < 32768 &&
@@ -2048,7 +2035,7 @@ int pick_draw_config(const csa_instance *I, bool general, DrawConfig &c) {
     if (const char *e = getenv("CSA_DRAW_KERNEL")) {
         // the register kernels are built for the shapes they win on only (solo F <= 16, lane F > 16)
         if (!general && !strcmp(e, "solo") && solo_ok) choice = 1;
-        else if (!general && (!strcmp(e, "lane") || !strcmp(e, "lanel")) && lane_ok && !solo_ok) choice = 2;
+        else if (!general && !strcmp(e, "lane") && lane_ok && !solo_ok) choice = 2;
         else if (!general && !strcmp(e, "wide") && wide_ok) choice = 8;
         else if (!general && !strcmp(e, "16") && g16_ok) choice = 16;
         else if (!general && !strcmp(e, "64")) choice = 64;
@@ -2077,13 +2064,6 @@ int pick_draw_config(const csa_instance *I, bool general, DrawConfig &c) {
         c.WPL = I->W <= 4 ? 4 : I->W <= 8 ? 8 : I->W <= 16 ? 16 : I->W <= 28 ? 28 : 32;
         c.fn = lane_fn(c.FPL, c.WPL);
         if (!c.fn) return fail(CSA_E_UNSUPPORTED, "no lane draw kernel for F=%d W=%d", I->F, I->W);
-        // the LDS-pool form where its pool fits (CSA_DRAW_KERNEL=lane|lanel picks one)
-        const char *e = getenv("CSA_DRAW_KERNEL");
-        const bool want_l = e ? !strcmp(e, "lanel") : kLanelDefault;
-        if (want_l && lanel_fn(c.FPL, c.WPL) && lanel_lds_bytes(c.FPL, c.WPL, I->n) <= 160 * 1024) {
-            c.lanel = true;
-            c.fn = lanel_fn(c.FPL, c.WPL);
-        }
         return CSA_OK;
     }
     c.FPL = pow2_ceil_int((I->F + c.G - 1) / c.G);
@@ -2225,18 +2205,16 @@ int launch_draw(const csa_instance *I, int32_t k, uint64_t seed, uint64_t panel_
     csa_instance *M = const_cast<csa_instance *>(I);  // the lane kernel's pick-list scratch
     if (d_picks_ext)
         A.picks16 = d_picks_ext;
-    // (the fused pack's chunked layout reserves whole workgroups of <= 512 panels)
-    else if (cfg.picks() && (rc = lane_picks(M, ((n_panels + 511) & ~511ull) * (uint64_t)((k + 7) & ~7), stream,
+    // (the fused pack's chunked layout reserves whole workgroups of <= 256 panels)
+    else if (cfg.picks() && (rc = lane_picks(M, ((n_panels + 255) & ~255ull) * (uint64_t)((k + 7) & ~7), stream,
                                              &A.picks16)))
         return rc;
-    const int threads = cfg.lanel  ? kLlThreads
-                        : cfg.lane ? kLaneThreads
+    const int threads = cfg.lane   ? kLaneThreads
                         : cfg.solo ? kSoloThreads
                         : cfg.wide ? kWideThreads
                                    : draw_threads(cfg.FPL, cfg.WPL);
     const int groups_wg = threads / cfg.G;
-    const size_t lds = cfg.lanel  ? lanel_lds_bytes(cfg.FPL, cfg.WPL, I->n)
-                       : cfg.lane ? lane_lds_bytes(cfg.FPL, cfg.WPL, I->n)
+    const size_t lds = cfg.lane   ? lane_lds_bytes(cfg.FPL, cfg.WPL, I->n)
                        : cfg.solo ? solo_lds_bytes(cfg.FPL, cfg.WPL, I->n)
                        : cfg.wide ? wide_lds_bytes(cfg.G, cfg.FPL, cfg.WPL)
                                   : draw_lds_bytes(cfg.G, cfg.FPL, cfg.WPL, I->W, k, groups_wg);
@@ -2744,8 +2722,6 @@ int csa_draw_kernel_name(const csa_instance *I, int32_t k, char *buf, uint64_t l
     if (rc) return rc;
     if (cfg.solo)
         snprintf(buf, (size_t)len, "draw_solo_kernel<%d, %d>", cfg.FPL, cfg.WPL);
-    else if (cfg.lanel)
-        snprintf(buf, (size_t)len, "draw_lanel_kernel<%d, %d>", cfg.FPL, cfg.WPL);
     else if (cfg.lane)
         snprintf(buf, (size_t)len, "draw_lane_kernel<%d, %d, %d>", cfg.FPL, cfg.WPL,
                  (cfg.WPL / 2 + CSA_LANE_SKDIV - 1) / CSA_LANE_SKDIV);

@@ -3,8 +3,7 @@
 The batch path picks draw_solo_kernel (1 lane per panel), draw_lane_kernel (2 lanes per
 panel) or draw_wide_kernel (8 lanes per panel, n up to 8192), all writing pick lists (packed
 in the draw's tail or by picks_pack_kernel), or draw_kernel (G = 16 / 64) from the instance
-shape; CSA_DRAW_KERNEL=solo|lane|lanel|wide|16|64 forces a layout the instance fits (lanel:
-draw_lanel_kernel, the two-lane kernel with its pool in LDS).  Each must give the
+shape; CSA_DRAW_KERNEL=solo|lane|wide|16|64 forces a layout the instance fits.  Each must give the
 oracle's panels and attempt counts bit-exactly, including the edge cases of
 legacy.py:124-200 (restarts, rejections, max = 0 features, max = 0 < min).
 """
@@ -43,7 +42,7 @@ def _sample(enc, k, S, seed, begin=0, max_attempts=0):
     return panels, attempts
 
 
-@pytest.mark.parametrize("group", ["solo", "lane", "lanel", "wide", 16, 64])
+@pytest.mark.parametrize("group", ["solo", "lane", "wide", 16, 64])
 @pytest.mark.parametrize("name,k,S,seed", [("sf_e_tight_110", 110, 3000, 5), ("pathological_5", 5, 4000, 2),
                                            ("rejecty_6", 6, 20000, 8), ("example_small_20", 20, 20000, 1),
                                            ("couples_panel_from_twenty_people_no_constraints_2", 2, 20000, 3),
@@ -79,7 +78,7 @@ def _weird_instance():
     return cats, agents
 
 
-@pytest.mark.parametrize("group", ["solo", "lane", "lanel", "wide", 16, 64])
+@pytest.mark.parametrize("group", ["solo", "lane", "wide", 16, 64])
 def test_zero_max_features_match_oracle(gpu_available, draw_group, group):
     """max = 0 features (dead, and max = 0 < min which routes to draw_kernel) vs the oracle."""
     P = pkg()
@@ -177,7 +176,7 @@ def test_k_zero_draws_empty_panels(gpu_available):
         _sample(enc, 0, 10, 3, max_attempts=5)
 
 
-@pytest.mark.parametrize("group", ["solo", "lane", "lanel"])
+@pytest.mark.parametrize("group", ["solo", "lane"])
 @pytest.mark.parametrize("case", PHILOX_CASES)
 def test_register_layouts_match_goldens(gpu_available, draw_group, group, case):
     """The one- and two-lane register kernels (fused pack included) against the reference goldens."""
@@ -298,28 +297,26 @@ def test_wide_layouts_match_oracle(gpu_available, F_per_cat, n, k, lo, hi, want)
                      "selection_errors": int(oatt.sum()) - S - int(rejects.sum())}
 
 
-@pytest.mark.parametrize("layout", ["lane", "lanel"])
 @pytest.mark.parametrize("F_per_cat,n,k,lo,hi,wn", [
     ((6, 6, 6), 1000, 80, 0.9, 1.1, 16),      # F = 18, W = 16
     ((6, 6, 6), 1000, 90, 0.97, 1.03, 16),    # restarts
     ((8, 8, 8, 6), 1700, 110, 0.9, 1.1, 28),  # F = 30, W = 27 (the sf_e shape)
     ((8, 8, 8, 6), 1650, 100, 0.96, 1.04, 28),
 ])
-def test_two_lane_layouts_match_oracle(gpu_available, draw_group, layout, F_per_cat, n, k, lo, hi, wn):
-    """draw_lane_kernel and draw_lanel_kernel (pool in LDS: 512 panels per 1024-thread workgroup, ragged
-    last workgroup) on synthetic pools with 16 < F <= 32, against the C oracle: panels, attempts and the
+def test_two_lane_layouts_match_oracle(gpu_available, F_per_cat, n, k, lo, hi, wn):
+    """draw_lane_kernel through the default routing on synthetic pools with 16 < F <= 32 (W = 16 and the
+    sf_e shape W = 26-27, with and without restarts), against the C oracle: panels, attempts and the
     restart counters."""
     import ctypes
     P = pkg()
     N = pkg("_native")
     A = pkg("analysis")
-    draw_group(layout)
     cats, agents, o = _synthetic_tight(F_per_cat, n, k, seed=n + k, lo=lo, hi=hi)
     enc = P.encode(cats, agents)
     buf = np.zeros(64, np.uint8)
     N.check(N.lib().csa_draw_kernel_name(enc.handle, k, buf.ctypes.data_as(ctypes.c_char_p), 64))
     name = bytes(buf).split(b"\0")[0].decode()
-    assert name.startswith("draw_%s_kernel<32, %d" % (layout, wn)), name
+    assert name.startswith("draw_lane_kernel<32, %d" % wn), name
     S, seed, begin = 2600, 9, 31337
     rejects = np.zeros(S, np.uint32)
     rc, opanels, oatt, _ = coracle.draw(o, k, seed, begin, S, max_attempts=100000, rejects=rejects)
