@@ -740,133 +740,6 @@ __global__ __launch_bounds__(kXtThreads) void xt_count_kernel(const uint64_t *__
         if (cnt[p]) atomicAdd(reinterpret_cast<unsigned long long *>(counts + p0 + p), (unsigned long long)cnt[p]);
 }
 
-// xt_wave_kernel<MODE>: the same transpose with no workgroup barrier in the block loop.  Every wave
-// owns a 64 x Wp-word LDS tile and a run of 64-panel blocks (wave wv of workgroup x: blocks
-// x*bpg + wv, + kXwWaves, ...); it loads a block with coalesced 8-byte loads (64 lanes = 512
-// contiguous bytes), keeps the next block's words in flight (32 per lane at most) while it
-// transposes the current one out of its tile, and keeps its agents' counts in registers (lane l,
-// column w: agent 64 w + l).  One barrier at the end merges the waves' counts in LDS before the
-// int64 atomics.  Output identical to xt_count_kernel.
-//   MODE 0  W <= 32, W odd:  the block is one flat run of 64 W words; tile stride Wp = W, so
-//           element e of the run sits in tile slot e (immediate LDS offsets);
-//   MODE 1  W <= 32, W even: the same run, tile stride W + 1 (conflict-free column reads), slot
-//           e + e / W (e / W by a multiply-shift: exact for e < 2048, W <= 32);
-//   MODE 2  W > 32: column range blockIdx.y = words [32 y, 32 y + CW) of each row, two 32-word row
-//           segments per load, tile stride 33.
-constexpr int kXwWaves = 4;
-template <int MODE>
-__global__ __launch_bounds__(64 * kXwWaves, 2) void xt_wave_kernel(const uint64_t *__restrict__ panels,
-                                                                   uint64_t S, int n, int W, int npad,
-                                                                   uint64_t *__restrict__ xt,
-                                                                   int64_t *__restrict__ counts, int bpg,
-                                                                   uint32_t wmagic) {
-    extern __shared__ uint64_t smem[];
-    const int c0 = (int)blockIdx.y * kXtCols, CW = min(kXtCols, W - c0);
-    const int Wp = MODE == 0 ? W : MODE == 1 ? W + 1 : kXtCols + 1;
-    const int p0 = 64 * c0, np = min(n - p0, 64 * CW);
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    uint64_t *tile = smem + wv * 64 * Wp;
-    const XtLane tc = xt_lane_consts(lane);
-    const int ncol = min(npad / 64 - c0, kXtCols);
-    const int nld = MODE == 2 ? 32 : W;  // 8-byte loads per lane per block
-    const int half = lane >> 5, lw = lane & 31;  // MODE 2: row parity / word of this lane
-    const uint64_t nblk = (S + 63) / 64;
-    const uint64_t bw0 = (uint64_t)blockIdx.x * bpg + wv, bend = min(nblk, (uint64_t)(blockIdx.x + 1) * bpg);
-    uint64_t pre[32];
-    auto load_blk = [&](uint64_t b) {
-        const uint64_t row0 = b * 64;
-        const int rows = (int)min<uint64_t>(64, S - row0);
-        const uint64_t *src = panels + row0 * (uint64_t)W + c0;
-        if (MODE != 2) {
-            const int lim = rows * W;  // valid words of the run
-            if (rows == 64) {
-#pragma unroll
-                for (int i = 0; i < 32; ++i)
-                    if (i < nld) pre[i] = src[lane + 64 * i];
-            } else {
-#pragma unroll
-                for (int i = 0; i < 32; ++i) {
-                    if (i < nld) {
-                        const int e = lane + 64 * i;
-                        const uint64_t v = src[e < lim ? e : 0];  // in range, zeroed below
-                        pre[i] = e < lim ? v : 0ull;
-                    }
-                }
-            }
-        } else {
-            // 32-bit word offsets from src (a block spans < 2^32 words); words past CW load a
-            // clamped in-range word and are zeroed.  The offset is opaque per block so the
-            // compiler steps it instead of keeping 32 hoisted 64-bit addresses live.
-            const bool okw = lw < CW;
-            uint32_t off = (uint32_t)(half * W + min(lw, CW - 1));
-            asm volatile("" : "+v"(off));
-            const uint32_t step = 2u * (uint32_t)W;
-            if (rows == 64) {
-#pragma unroll
-                for (int i = 0; i < 32; ++i) {
-                    const uint64_t v = src[off + (uint32_t)i * step];
-                    pre[i] = okw ? v : 0ull;
-                }
-            } else {
-                const uint32_t last = (uint32_t)(rows - 1) * (uint32_t)W + (uint32_t)min(lw, CW - 1);
-#pragma unroll
-                for (int i = 0; i < 32; ++i) {
-                    const int row = 2 * i + half;
-                    const uint64_t v = src[row < rows ? off + (uint32_t)i * step : last];
-                    pre[i] = (row < rows && okw) ? v : 0ull;
-                }
-            }
-        }
-    };
-    uint32_t cnt[kXtCols];
-#pragma unroll
-    for (int w = 0; w < kXtCols; ++w) cnt[w] = 0;
-    if (bw0 < bend) load_blk(bw0);
-    for (uint64_t b = bw0; b < bend; b += kXwWaves) {
-        if (MODE == 0) {
-#pragma unroll
-            for (int i = 0; i < 32; ++i)
-                if (i < nld) tile[lane + 64 * i] = pre[i];
-        } else if (MODE == 1) {
-            uint32_t lm = (uint32_t)lane * wmagic;
-            asm volatile("" : "+v"(lm));  // recomputed per block, not 32 live row registers
-#pragma unroll
-            for (int i = 0; i < 32; ++i)
-                if (i < nld) tile[lane + 64 * i + (int)((lm + (uint32_t)(64 * i) * wmagic) >> 17)] = pre[i];
-        } else {
-#pragma unroll
-            for (int i = 0; i < 32; ++i) tile[(2 * i + half) * (kXtCols + 1) + lw] = pre[i];
-        }
-        if (b + kXwWaves < bend) load_blk(b + kXwWaves);  // in flight while this block is transposed
-        uint32_t *x32 = xt ? reinterpret_cast<uint32_t *>(xt) + 2 * b * (uint64_t)npad + p0 + lane : nullptr;
-#pragma unroll
-        for (int w = 0; w < kXtCols; ++w) {
-            if (w < ncol) {
-                const uint64_t x = w < CW ? tile[lane * Wp + w] : 0ull;
-                uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
-                wave_transpose64(lo, hi, tc);
-                if (x32) {  // two 32-bit planes per panel block, as xt_count_kernel
-                    x32[64 * w] = lo;
-                    x32[64 * w + npad] = hi;
-                }
-                cnt[w] += (uint32_t)(__popc(lo) + __popc(hi));
-            }
-        }
-    }
-    __syncthreads();  // every wave is done with its tile: the count array aliases the tiles
-    uint32_t *csum = reinterpret_cast<uint32_t *>(smem);
-    for (int p = threadIdx.x; p < np; p += blockDim.x) csum[p] = 0;
-    __syncthreads();
-#pragma unroll
-    for (int w = 0; w < kXtCols; ++w) {
-        const int p = 64 * w + lane;
-        if (w < ncol && p < np && cnt[w]) atomicAdd(&csum[p], cnt[w]);
-    }
-    __syncthreads();
-    for (int p = threadIdx.x; p < np; p += blockDim.x)
-        if (csum[p]) atomicAdd(reinterpret_cast<unsigned long long *>(counts + p0 + p), (unsigned long long)csum[p]);
-}
-
 // ------------------------------------------------------------------------------------------
 // Pair counts: X^T X on MFMA (PairHistogram.add_portfolio_of_panels_to_histogram, analysis.py:90-95)
 // ------------------------------------------------------------------------------------------
@@ -2734,11 +2607,6 @@ int csa_draw_kernel_name(const csa_instance *I, int32_t k, char *buf, uint64_t l
 
 int32_t csa_xt_pad(int32_t n) { return ((n + kPairBlock - 1) / kPairBlock) * kPairBlock; }
 
-// xt_wave_kernel by default for narrow panels only (tools/xt_bench.py, 10^6 panels: W = 4 0.039 vs 0.054 ms;
-// W = 27 0.109 vs 0.113; W = 32 0.126 vs 0.120; W = 128 0.418 vs 0.395 -- the barrier-per-block kernel
-// keeps more loads in flight per CU once a block is wide)
-inline bool xt_wave_default(int W) { return W <= 8; }
-
 int csa_transpose_count_async(const uint64_t *d_panels, uint64_t n_panels, int32_t n, uint64_t *d_xt,
                               int64_t *d_counts, void *stream) {
     if (n <= 0 || !d_panels || !d_counts) return fail(CSA_E_INVALID, "transpose: bad arguments");
@@ -2756,28 +2624,6 @@ int csa_transpose_count_async(const uint64_t *d_panels, uint64_t n_panels, int32
         if (hipGetDevice(&dev) != hipSuccess ||
             hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
             cus = 256;
-    }
-    const char *xk = getenv("CSA_XT_KERNEL");  // "wave" | "lds" (the barrier-per-block xt_count_kernel)
-    if (xk ? !strcmp(xk, "wave") : xt_wave_default(W)) {
-        // xt_wave_kernel: one pass of workgroups (two per CU: 4 tiles of <= 17 KB each), blocks
-        // per workgroup a multiple of the wave count
-        const uint64_t per = std::max<uint64_t>(1, (nblk * ranges + 2 * (uint64_t)cus - 1) / (2 * (uint64_t)cus));
-        const uint64_t bpg = (per + kXwWaves - 1) / kXwWaves * kXwWaves;
-        const unsigned grid = (unsigned)((nblk + bpg - 1) / bpg);
-        const int mode = W > kXtCols ? 2 : (W & 1) ? 0 : 1;
-        const int wp = mode == 0 ? W : mode == 1 ? W + 1 : kXtCols + 1;
-        const size_t lds_w = (size_t)kXwWaves * 64 * wp * 8;
-        const uint32_t wmagic = (131072u + (uint32_t)W - 1) / (uint32_t)W;
-        const void *fn = mode == 0   ? reinterpret_cast<const void *>(&xt_wave_kernel<0>)
-                         : mode == 1 ? reinterpret_cast<const void *>(&xt_wave_kernel<1>)
-                                     : reinterpret_cast<const void *>(&xt_wave_kernel<2>);
-        const uint64_t np64 = n_panels;
-        const int npad = csa_xt_pad(n), ibpg = (int)bpg;
-        void *args[] = {(void *)&d_panels, (void *)&np64, (void *)&n, (void *)&W, (void *)&npad,
-                        (void *)&d_xt, (void *)&d_counts, (void *)&ibpg, (void *)&wmagic};
-        HIPCHK(hipLaunchKernel(fn, dim3(grid, ranges), dim3(64 * kXwWaves), args, lds_w, (hipStream_t)stream));
-        HIPCHK(hipGetLastError());
-        return CSA_OK;
     }
     const uint64_t bpg = std::max<uint64_t>(1, std::min<uint64_t>(kXtBlocksPerGroup, nblk * ranges / (2 * (uint64_t)cus)));
     const unsigned grid = (unsigned)((nblk + bpg - 1) / bpg);

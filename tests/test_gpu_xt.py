@@ -1,11 +1,10 @@
-"""GPU parity of the bit transpose + per-person counts (csa_transpose_count_async: the Counter of
-analysis.py:179,187 and the XT operand of PairHistogram, analysis.py:90-95) through the C ABI.
+"""GPU parity of the bit transpose + per-person counts (csa_transpose_count_async, xt_count_kernel: the
+Counter of analysis.py:179,187 and the XT operand of PairHistogram, analysis.py:90-95) through the C ABI.
 
-Both kernels -- xt_wave_kernel (CSA_XT_KERNEL=wave: wave-private tiles, three addressing modes: W odd,
-W even, W > 32 in 32-word column ranges) and xt_count_kernel (CSA_XT_KERNEL=lds) -- against a numpy
-restatement on the same packed panels: XT plane layout (xt32[b][0][p] = panels 64b..64b+31 of agent p,
-xt32[b][1][p] = panels 64b+32..64b+63, zero past n up to csa_xt_pad(n)) and counts added onto the
-prior contents.  Ragged last blocks, fewer blocks than waves, partial column ranges.  Bar: bit-exact.
+Against a numpy restatement on the same packed panels: XT plane layout (xt32[b][0][p] = panels 64b..64b+31
+of agent p, xt32[b][1][p] = panels 64b+32..64b+63, zero past n up to csa_xt_pad(n)) and counts added onto
+the prior contents.  Ragged last blocks, fewer blocks than workgroups, odd / even W, 32-word column ranges
+with a partial last range.  Bar: bit-exact.
 """
 import numpy as np
 import pytest
@@ -29,17 +28,11 @@ def _ref(panels, S, n, npad):
     return xt, counts
 
 
-@pytest.fixture(params=["wave", "lds"])
-def xt_kernel(request, monkeypatch):
-    monkeypatch.setenv("CSA_XT_KERNEL", request.param)
-    return request.param
-
-
 @pytest.mark.parametrize("n,S", [(1727, 20000), (1727, 1), (1727, 63), (2000, 6401), (200, 3000), (64, 130),
                                  (40, 257), (1000, 64 * 4 * 3 + 5), (2050, 1000), (2100, 777), (8192, 4097),
                                  (8192, 64), (4500, 300), (2048, 2048)])
 @pytest.mark.parametrize("with_xt", [True, False])
-def test_transpose_count_exact(gpu_available, xt_kernel, n, S, with_xt):
+def test_transpose_count_exact(gpu_available, n, S, with_xt):
     import torch
     N = pkg("_native")
     L = N.lib()

@@ -1,9 +1,9 @@
-"""Bit transpose + counts microbenchmark on the GPU box: csa_transpose_count_async on random packed
-panels (k of n bits set per panel, like a LEGACY draw) for each kernel (xt_wave_kernel, CSA_XT_KERNEL=wave;
-xt_count_kernel, CSA_XT_KERNEL=lds), timed with HIP events on the launch stream; both kernels' XT and
-counts must be equal.  Bytes = the algorithmic 8 W B read + 8 npad / 64 B written per panel.
+"""Bit transpose + counts microbenchmark on the GPU box: csa_transpose_count_async (xt_count_kernel) on
+random packed panels alone, timed with HIP events on the launch stream, for several pool sizes.  Bytes =
+the algorithmic 8 W B read + 8 npad / 64 B written per panel.  CSA_XT_KERNEL selected variants in
+round 4 (profiles/r04_xt_ab/); --variants keeps that interface for a library that has them.
 
-    python tools/xt_bench.py [--n 1727,2000,8192] [--panels 1000000] [--reps 10]
+    python tools/xt_bench.py [--n 1727,2000,200,8192] [--panels 1000000] [--reps 10]
 """
 import argparse
 import ctypes
@@ -21,7 +21,7 @@ def main():
     ap.add_argument("--n", default="1727,2000,200,8192")
     ap.add_argument("--panels", type=int, default=10 ** 6)
     ap.add_argument("--reps", type=int, default=10)
-    ap.add_argument("--variants", default="wave,lds")
+    ap.add_argument("--variants", default="default")
     args = ap.parse_args()
     import torch
     N = importlib.import_module("citizensassemblies-replication_amd._native")
@@ -41,7 +41,8 @@ def main():
         nbytes = S * 8 * W + nblk * 8 * npad
         ref = None
         for var in args.variants.split(","):
-            os.environ["CSA_XT_KERNEL"] = var
+            if var != "default":
+                os.environ["CSA_XT_KERNEL"] = var
             xt = torch.empty(nblk * npad, dtype=torch.int64, device="cuda")
             cnt = torch.zeros(n, dtype=torch.int64, device="cuda")
             times = []
