@@ -1166,6 +1166,15 @@ __global__ __launch_bounds__(kP2Threads, NB == 4 ? 1 : 2) void pair_fp4_tile_ker
                 read_blk(j + 2, rwa, rwb);
                 expand(rna, rnb, fna, fnb);
                 mfma(fca, fcb);
+                // one MFMA, then its share of the expansion VALU (NB = 4: 56 VALU for 16 MFMAs; NB = 2: 42
+                // for 8): an MFMA holds the wave's issue for 8 of its 32 cycles and this wave is alone on
+                // its SIMD, so the fillers must sit in the gaps, not in runs (the compiler's own order left
+                // runs of 7 VALU and of 7 bare MFMAs: 10.3 -> 8.7 ms at NB = 4, 13.4 -> 11.9 at NB = 2)
+#pragma unroll
+                for (int q = 0; q < 4 * NB; ++q) {
+                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+                    __builtin_amdgcn_sched_group_barrier(0x002, NB == 4 ? 4 : 5, 0);  // VALU
+                }
                 __builtin_amdgcn_sched_barrier(0);
             };
             int j = 0;
@@ -1173,7 +1182,8 @@ __global__ __launch_bounds__(kP2Threads, NB == 4 ? 1 : 2) void pair_fp4_tile_ker
                 step(j, f0a, f0b, r1a, r1b, f1a, f1b, r0a, r0b);
                 step(j + 1, f1a, f1b, r0a, r0b, f0a, f0b, r1a, r1b);
             }
-            if (j < nb) step(j, f0a, f0b, r1a, r1b, f1a, f1b, r0a, r0b);
+            // an odd last block: its fragments are expanded and nothing is left to fetch or read
+            if (j < nb) mfma(f0a, f0b);
         }
         int rloc = 128 * wr + 4 * h, cloc = BC * wc + r32;
         asm volatile("" : "+v"(rloc), "+v"(cloc));
@@ -2690,10 +2700,12 @@ bool pair2_plan(int32_t n, uint64_t n_blocks, uint32_t engine, bool shared, Pair
     int cus = 256, dev = 0;
     if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     if (cus < kP2Xcds || cus % kP2Xcds) return false;
-    // B fragments per wave: 2 (256-register waves) when the launch shares the CUs with draws
-    // (CSA_PAIR_SHARED), else 4; CSA_P2_NB=2|4 forces either (A/B)
+    // B fragments per wave: 4 (512-register waves, one per SIMD) also when the launch shares the CUs with
+    // draws (CSA_PAIR_SHARED): with the interleaved loop it beats the 256-register NB = 2 form beside the
+    // n = 8192 draw (32.9 vs 31.7 M panels/s end to end); CSA_P2_NB=2|4 forces either (A/B)
+    (void)shared;
     const char *enb = getenv("CSA_P2_NB");
-    const int nbf = enb ? atoi(enb) : (shared ? 2 : 4);
+    const int nbf = enb ? atoi(enb) : 4;
     q.M.halves = nbf == 2 ? 2 : 1;
     q.M.nbt = csa_xt_pad(n) / kPairBlock;
     q.M.ntri = q.M.nbt * (q.M.nbt + 1) / 2;
