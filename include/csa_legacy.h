@@ -254,9 +254,9 @@ int csa_transpose_count_async(const uint64_t *d_panels, uint64_t n_panels, int32
  * scratch the call zero-fills d_pairs first), so a caller that counts each batch
  * afresh needs no n*n zero-fill of its own.  engine | CSA_PAIR_SHARED is a
  * scheduling hint, never a change of result: the launch will share the CUs with
- * concurrent draw kernels (a pipelined caller), so the per-CU kernel takes its
- * 256-register form (128 x 64 wave tiles) that leaves room for a draw workgroup
- * beside it, instead of the 512-register form that is faster alone. */
+ * concurrent draw kernels (a pipelined caller).  The library currently takes the
+ * same 512-register per-CU form either way (measured faster beside the draws than
+ * the 256-register form, which CSA_P2_NB=2 still selects). */
 #define CSA_PAIR_FP4 0u
 #define CSA_PAIR_I8 1u
 #define CSA_PAIR_OVERWRITE 0x100u
