@@ -63,6 +63,9 @@ def parse():
                     help="serialise every stage on one stream (default: draws on their own stream, "
                          "--bufs - 1 steps ahead of the counting)")
     ap.add_argument("--bufs", type=int, default=3, help="panel buffers of the draw/count pipeline")
+    ap.add_argument("--draw-streams", type=int, default=int(os.environ.get("CSA_DRAW_STREAMS", "1")),
+                    help="streams the draws of consecutive steps alternate over (A/B only: > 1 needs a library "
+                         "with a pick-list ring, profiles/r04f_draw_streams/, and measured slower)")
     ap.add_argument("--pack-on", default="fused", choices=("fused", "draw", "count"),
                     help="where pick lists become panels: inside the draw kernel (fused, default), "
                          "picks_pack_kernel after the draw on the draw stream, or first on the counting "
@@ -309,7 +312,7 @@ def run_job(args, world, rank, dev, torch, dist, A, Dd, enc, k, S, inst_dir, pip
     b0, e0 = Dd.shard_range(Pj, world, rank)
     share, n_max = e0 - b0, Dd.shard_range(Pj, world, 0)[1]
     W = enc.W
-    draw_stream = torch.cuda.Stream(dev)
+    draw_streams = [torch.cuda.Stream(dev) for _ in range(max(args.draw_streams, 1))]
     panels_all = torch.empty(max(share * W, 1), dtype=torch.int64, device=dev)
     hashes_all = torch.empty(max(2 * share, 2), dtype=torch.int64, device=dev)
     table = Dd.HashTable(max(share, 1), dev) if world == 1 else None
@@ -327,9 +330,10 @@ def run_job(args, world, rank, dev, torch, dist, A, Dd, enc, k, S, inst_dir, pip
         for j in range(steps):
             o, ln = j * S, min(S, count - j * S)
             pipe.panels, pipe.hashes = panels_all[o * W:(o + ln) * W], hashes_all[2 * o:2 * (o + ln)]
-            pipe.draw(args.seed, begin + o, ln, stream=draw_stream)
+            ds = draw_streams[j % len(draw_streams)]
+            pipe.draw(args.seed, begin + o, ln, stream=ds)
             ev = torch.cuda.Event()
-            ev.record(draw_stream)
+            ev.record(ds)
             drawn.append(ev)
         for j in range(steps):
             o, ln = j * S, min(S, count - j * S)
@@ -470,7 +474,7 @@ def main():
     overlap = not args.no_overlap
     nb = max(args.bufs, 2) if overlap else 1
     ahead = nb - 1                                  # draws enqueued ahead of the counting
-    draw_stream = torch.cuda.Stream(dev) if overlap else stream
+    draw_streams = [torch.cuda.Stream(dev) for _ in range(max(args.draw_streams, 1))] if overlap else [stream]
     pbufs = [pipe.panels] + [torch.empty_like(pipe.panels) for _ in range(nb - 1)]
     hbufs = [pipe.hashes] + [torch.empty_like(pipe.hashes) for _ in range(nb - 1)]
     pack_on_count = split and args.pack_on == "count"
@@ -489,7 +493,7 @@ def main():
 
     def enqueue_draw(j, rec):
         b = j % nb
-        ds = stream if mode["serial"] else draw_stream
+        ds = stream if mode["serial"] else draw_streams[j % len(draw_streams)]
         ds.wait_event(counted[b])                 # step j - nb is done reading this buffer
         pipe.panels, pipe.hashes = pbufs[b], hbufs[b]
         if pack_on_count:

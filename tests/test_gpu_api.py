@@ -171,6 +171,43 @@ def test_draw_stats_k0(gpu_available):
     assert A.draw_stats(enc) == {"attempts": 500, "selection_errors": 0, "rejections": 0}
 
 
+@pytest.mark.parametrize("name,k,S,chunk", [("sf_e_tight_110", 110, 20011, 3000), ("sf_e_110", 110, 9000, 2048),
+                                            ("synthetic8192_200", 200, 2600, 1000), ("rejecty_6", 6, 5000, 700)])
+def test_sample_device_chunks_overlapped(gpu_available, name, k, S, chunk):
+    """legacy_sample_device in chunks: every chunk's draw enqueued at once on the draw stream, the
+    counting following chunk by chunk on the pipeline stream -- counts, pairs, the exact distinct
+    count, the panels and the draw statistics equal one single-chunk batch of the same panel indices."""
+    import torch
+    A = pkg("analysis")
+    inst = _inst(name, k)
+    enc = pkg().encode(inst.categories, inst.agents)
+    one = A.legacy_sample_device(enc, k, S, 5, chunk=S)
+    enc2 = pkg().encode(inst.categories, inst.agents)
+    many = A.legacy_sample_device(enc2, k, S, 5, chunk=chunk)
+    torch.cuda.synchronize()
+    assert np.array_equal(one.counts, many.counts)
+    assert torch.equal(torch.triu(one.pairs), torch.triu(many.pairs))
+    assert one.unique == many.unique
+    assert torch.equal(one.panels, many.panels)
+    assert one.stats == many.stats and one.stats["attempts"] >= S
+
+
+@pytest.mark.parametrize("name,k,S,chunk", [("sf_e_tight_110", 110, 12007, 2500), ("synthetic8192_200", 200, 2600, 640)])
+def test_legacy_sample_c_pipeline_chunks(gpu_available, monkeypatch, name, k, S, chunk):
+    """csa_legacy_sample's own pipeline (C ABI) in chunks of CSA_SAMPLE_CHUNK panels (chunk c + 1
+    drawn while chunk c is counted and paired): equal to one single-chunk batch."""
+    A = pkg("analysis")
+    inst = _inst(name, k)
+    enc = pkg().encode(inst.categories, inst.agents)
+    one = A.legacy_sample_raw(enc, k, S, 9)
+    monkeypatch.setenv("CSA_SAMPLE_CHUNK", str(chunk))
+    many = A.legacy_sample_raw(enc, k, S, 9)
+    assert np.array_equal(one.counts, many.counts)
+    assert np.array_equal(np.triu(one.pairs), np.triu(many.pairs))
+    assert one.unique == many.unique and np.array_equal(one.panels, many.panels)
+    assert one.stats == many.stats
+
+
 def test_exchange_local_distinct_beyond_partitioned_path(gpu_available):
     """csa_exchange_pack_async on 8192 x 2048 + 4096 entries (the partitioned dedupe's limit + 1
     block): the global-table fallback lists exactly one index per distinct panel."""
