@@ -368,34 +368,20 @@ def legacy_sample_device(enc, k, S, random_seed, keep_panels=True, chunk=1 << 20
         own_p, own_h, own_pairs = pipe.panels, pipe.hashes, pipe.pairs
         pipe.pairs = pairs
         try:
-            chunks = [(off, min(C, S - off)) for off in range(0, S, C)]
-            drawn = []
             if host_panels is None:
-                # every chunk's draw is enqueued at once on one draw stream (each chunk has its own
-                # slice of the batch's panel and hash tensors), and the counting of chunk c on the
-                # pipeline stream waits only for chunk c's draw: the counting kernels of chunk c share
-                # the CUs with the draw of chunk c + 1 (bench.py's pipeline).  Two draw streams were
-                # measured slower (profiles/r04f_draw_streams/).
-                st = getattr(pipe, "draw_stream", None)
-                if st is None:
-                    st = pipe.draw_stream = torch.cuda.Stream(dev)
-                st.wait_stream(pipe.stream)    # after the resets above
-                for off, ln in chunks:
+                # chunk draws on the pipeline's draw stream, counting and pairs on its stream, overlapped
+                # (DevicePipeline.draw_count_chunks); two draw streams were measured slower
+                # (profiles/r04f_draw_streams/)
+                pipe.draw_count_chunks(random_seed, 0, S, panels, hashes, C, overwrite_pairs=True)
+            else:
+                for off in range(0, S, C):
+                    ln = min(C, S - off)
                     pipe.panels, pipe.hashes = panels[off * W:(off + ln) * W], hashes[2 * off:2 * (off + ln)]
-                    pipe.draw(random_seed, off, ln, stream=st)
-                    ev = torch.cuda.Event()
-                    ev.record(st)
-                    drawn.append(ev)
-            for j, (off, ln) in enumerate(chunks):
-                pipe.panels, pipe.hashes = panels[off * W:(off + ln) * W], hashes[2 * off:2 * (off + ln)]
-                if host_panels is None:
-                    pipe.stream.wait_event(drawn[j])
-                else:
                     src = np.ascontiguousarray(host_panels[off:off + ln], np.uint64).view(np.int64).reshape(-1)
                     pipe.panels.copy_(torch.from_numpy(src), non_blocking=False)
                     pipe.hash(ln)
-                pipe.transpose_count(ln)
-                pipe.pair_counts(ln, overwrite=off == 0, shared=j + 1 < len(chunks))
+                    pipe.transpose_count(ln)
+                    pipe.pair_counts(ln, overwrite=off == 0)
             if S == 0:
                 pairs.zero_()
             table = getattr(enc, "_table", None)

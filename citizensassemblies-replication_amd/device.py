@@ -141,6 +141,39 @@ class DevicePipeline:
                                          N.ptr(self.table), self.slots, N.ptr(self.unique), N.ptr(self.status),
                                          _stream_ptr(self.stream)))
 
+    def draw_count_chunks(self, seed, panel_begin, S, panels, hashes, chunk, overwrite_pairs=False):
+        """Draw S panels (global indices panel_begin ..) into ``panels`` / ``hashes`` (tensors of the
+        whole batch) and accumulate their counts and pairs, in chunks of at most ``chunk`` panels
+        (at most max_panels): every chunk's draw is enqueued at once on the pipeline's draw stream, each into
+        its own slice, and the pipeline stream counts and pairs chunk c after chunk c's draw event --
+        beside the draw of chunk c + 1 (bench.py's pipeline).  The first chunk stores its pair counts
+        with ``overwrite_pairs``; later chunks add theirs.  Ordered after everything already on the
+        pipeline stream; on return the pipeline stream is ordered after every draw."""
+        import torch
+        S, C, W = int(S), max(1, min(int(chunk), self.max_panels)), self.enc.W
+        chunks = [(off, min(C, S - off)) for off in range(0, S, C)]
+        st = getattr(self, "draw_stream", None)
+        if st is None:
+            st = self.draw_stream = torch.cuda.Stream(self.device)
+        st.wait_stream(self.stream)
+        own_p, own_h = self.panels, self.hashes
+        try:
+            drawn = []
+            for off, ln in chunks:
+                self.panels, self.hashes = panels[off * W:(off + ln) * W], hashes[2 * off:2 * (off + ln)]
+                self.draw(seed, panel_begin + off, ln, stream=st)
+                ev = torch.cuda.Event()
+                ev.record(st)
+                drawn.append(ev)
+            for j, (off, ln) in enumerate(chunks):
+                self.stream.wait_event(drawn[j])
+                self.panels = panels[off * W:(off + ln) * W]
+                self.transpose_count(ln)
+                if self.want_pairs:
+                    self.pair_counts(ln, overwrite=overwrite_pairs and j == 0, shared=j + 1 < len(chunks))
+        finally:
+            self.panels, self.hashes = own_p, own_h
+
     def run(self, seed, panel_begin, S, max_attempts=0, overwrite_pairs=False):
         """Enqueue the whole pass; results accumulate into counts / pairs / unique (pairs are
         stored instead with ``overwrite_pairs``)."""

@@ -487,9 +487,10 @@ def legacy_probabilities_distributed(instance, iterations, random_seed, keep_pan
     pipe.reset()
     A.reset_draw_stats(enc, pipe.stream)
     if local:
-        pipe.draw(random_seed, begin, local)
-        pipe.transpose_count(local)
-        pipe.pair_counts(local)
+        # the shard in chunks (default 2^20 panels; CSA_SHARD_CHUNK), each chunk's counting and pairs
+        # beside the next chunk's draw
+        pipe.draw_count_chunks(random_seed, begin, local, pipe.panels, pipe.hashes,
+                               int(os.environ.get("CSA_SHARD_CHUNK", 1 << 20)))
     _raise_together(pipe.status, pipe.stream)
     counts, pairs, u = combine(pipe.counts, pipe.pairs, pipe.hashes[: 2 * local], pipe.panels[: local * enc.W],
                                enc.W, pair_bound=S, status=pipe.status, redraw=(enc.handle, instance.k, random_seed, 0),

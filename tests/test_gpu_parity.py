@@ -537,16 +537,19 @@ def _dist_worker(rank, world, port, out_dir, name, k, S, seed):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("name,k,S,seed", [("sf_e_110", 110, 9001, 3),
-                                           ("couples_panel_from_twenty_people_no_constraints_2", 2, 5000, 1)])
-def test_legacy_probabilities_distributed_gloo(gpu_available, tmp_path, name, k, S, seed):
+@pytest.mark.parametrize("name,k,S,seed,chunk", [("sf_e_110", 110, 9001, 3, 0), ("sf_e_110", 110, 9001, 4, 1700),
+                                                 ("couples_panel_from_twenty_people_no_constraints_2", 2, 5000, 1, 0)])
+def test_legacy_probabilities_distributed_gloo(gpu_available, tmp_path, monkeypatch, name, k, S, seed, chunk):
     """analysis.legacy_probabilities with a 2-rank process group (both ranks on this GPU, gloo:
-    RCCL refuses two ranks on one device): the sharded draw, the exact panel exchange and the
+    RCCL refuses two ranks on one device): the sharded draw (``chunk``: each rank's shard drawn in
+    chunks of that many panels, counted beside the next chunk's draw), the exact panel exchange and the
     found_panels -- gathered to rank 0 only when iterated / pickled (no dist.recv before), `in`,
     and the pickled tuple -- equal the single-GPU result."""
     import socket
     import torch.multiprocessing as mp
     A = pkg("analysis")
+    if chunk:
+        monkeypatch.setenv("CSA_SHARD_CHUNK", str(chunk))
     with socket.socket() as sk:
         sk.bind(("127.0.0.1", 0))
         port = sk.getsockname()[1]
