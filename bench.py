@@ -63,6 +63,8 @@ def parse():
                     help="serialise every stage on one stream (default: draws on their own stream, "
                          "--bufs - 1 steps ahead of the counting)")
     ap.add_argument("--bufs", type=int, default=3, help="panel buffers of the draw/count pipeline")
+    ap.add_argument("--count-priority", type=int, default=int(os.environ.get("CSA_COUNT_PRIORITY", "0")),
+                    help="1: counting stream at the highest stream priority (A/B)")
     ap.add_argument("--draw-streams", type=int, default=int(os.environ.get("CSA_DRAW_STREAMS", "1")),
                     help="streams the draws of consecutive steps alternate over (A/B only: > 1 needs a library "
                          "with a pick-list ring, profiles/r04f_draw_streams/, and measured slower)")
@@ -455,6 +457,10 @@ def main():
     enc.check_quotas(k)
     want_pairs = not args.no_pairs
     stream = torch.cuda.current_stream(dev)
+    if args.count_priority:
+        # the counting / exchange stream at the highest priority: its workgroups dispatch before the
+        # draws' when both wait for CU slots (A/B with --draw-streams > 1)
+        stream = torch.cuda.Stream(dev, priority=torch.cuda.Stream.priority_range()[1])
     engine_id, engine_peak, engine_desc = PAIR_ENGINES[args.pair_engine]
     pipe = Dv.DevicePipeline(enc, k, S, want_pairs=want_pairs, want_unique=True, device=dev, stream=stream,
                              pair_engine=engine_id)
