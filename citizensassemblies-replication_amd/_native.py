@@ -53,6 +53,7 @@ SIGNATURES = {
     "csa_legacy_find": (ctypes.c_int, [_P, _I32, _U64, _U64, _U64, _U32, _P, _P]),
     "csa_legacy_attempt": (ctypes.c_int, [_P, _I32, _U64, _U64, _U32, _P, _P, _P, _P, _P]),
     "csa_first_panel_not_in": (ctypes.c_int, [_P, _I32, _U64, _U64, _U64, _U32, _P, _U64, _U64, _P, _P]),
+    "csa_draw_round_panels": (ctypes.c_int, [_P, _I32, _P]),
     "csa_draw_async": (ctypes.c_int, [_P, _I32, _U64, _U64, _U64, _U32, _P, _P, _P, _P, _P, _P]),
     "csa_picks_stride": (_I32, [_I32]),
     "csa_draw_picks_supported": (ctypes.c_int, [_P, _I32]),
@@ -72,12 +73,14 @@ SIGNATURES = {
     "csa_exchange_pack_async": (ctypes.c_int, [_P, _P, _U64, _I32, _U32, _U64, _P, _U64, _P, _P, _P, _P, _P]),
     "csa_pairs_pack_async": (ctypes.c_int, [_P, _I32, _P, _P]),
     "csa_pairs_unpack_async": (ctypes.c_int, [_P, _I32, _P, _P]),
+    "csa_pairs_upper_async": (ctypes.c_int, [_P, _I32, ctypes.c_double, _P, _P]),
     "csa_status_decode": (ctypes.c_int, [_P]),
     "csa_legacy_draw_mt": (ctypes.c_int, [_I32, _I32, _I32, _P, _P, _P, _P, _P, _P, _P, _I32, _P, _U64, _U32,
                                           _I32, _P, _P, _P, _P, _P, _P, _P]),
     "csa_instance_set_address": (ctypes.c_int, [_P, _P]),
     "csa_instance_draw_stats": (ctypes.c_int, [_P, _I32, _P]),
     "csa_instance_draw_stats_reset": (ctypes.c_int, [_P, _P]),
+    "csa_instance_draw_stats_async": (ctypes.c_int, [_P, _P, _P]),
     "csa_exchange_keys_async": (ctypes.c_int, [_P, _P, _U64, _I32, _U64, _U32, _U64, _P, _U64, _P, _P, _P, _P]),
     "csa_unique_keys_scratch_bytes": (_U64, [_U64, _I32]),
     "csa_unique_keys_async": (ctypes.c_int, [_P, _I32, _U64, _U32, _P, _U32, _U64, _P, _P, _U64, _P, _P, _P]),

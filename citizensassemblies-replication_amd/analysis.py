@@ -32,51 +32,84 @@ ProbAllocation = Dict
 
 
 class PairHistogram:
-    """analysis.py:68-98 with a dense backing store.
+    """analysis.py:68-98 with a packed backing store.
 
-    The (n, n) matrix's strict upper triangle holds the pair values (row-major
-    i < j is the reference's key order, analysis.py:70); the lower triangle is
-    ignored.  Integer counts stay exact until
-    ``turn_into_probabilities_by_dividing_all_elements_by_given_number``
-    divides them (float64 true division, as the reference's ``/``).  A
-    histogram built by ``legacy_probabilities`` keeps the device's integer
-    pair counts and materialises the host matrix (one copy + the division) on
-    first access, so a caller that only reads per-person probabilities or
-    ``len(found_panels)`` never moves the n*n matrix.
+    The reference keeps a dict of the n(n-1)/2 pairs i < j in row-major key order
+    (analysis.py:70); here the same values sit in one array ``_u`` of that length and
+    order (strict upper triangle, row-major: pair (i, j) at i(n-1) - i(i-1)/2 + j-i-1).
+    Integer counts stay exact until
+    ``turn_into_probabilities_by_dividing_all_elements_by_given_number`` divides them
+    (float64 true division, as the reference's ``/``).  A histogram built by
+    ``legacy_probabilities`` keeps the device's n*n integer pair counts and materialises
+    ``_u`` on first access: the triangle is packed and divided on the device
+    (csa_pairs_upper_async) and only its n(n-1)/2 float64 values cross PCIe, so a caller
+    that only reads per-person probabilities or ``len(found_panels)`` never moves it.
     """
 
     def __init__(self, number_of_agents, uniform_distribution=False, counts=None):
         n = int(number_of_agents)
         self.n = n
-        self._src = None        # lazily materialised integer counts (numpy or device tensor)
+        self._src = None        # lazily materialised integer counts: n*n numpy array or device tensor
         self._divs = []         # divisions pending on _src, applied in order at materialisation
-        self._mat = None
+        self._uv = None
         if counts is not None:
             if hasattr(counts, "device") and not isinstance(counts, np.ndarray):
                 self._src = counts
             else:
-                self._mat = np.asarray(counts)
-                assert self._mat.shape == (n, n)
+                c = np.asarray(counts)
+                assert c.shape == (n, n)
+                self._src = c
         else:
-            self._mat = np.zeros((n, n), np.int64)
+            self._uv = np.zeros(n * (n - 1) // 2, np.int64)
         self._counts = self._S = None   # integer pair counts and S when built by finish()
         if uniform_distribution:
             npairs = n * (n - 1) // 2
             self._src = None
-            self._mat = np.full((n, n), 1 / npairs if npairs else 0.0, np.float64)
+            self._uv = np.full(npairs, 1 / npairs if npairs else 0.0, np.float64)
+
+    def _materialise_device(self):
+        """Strict upper triangle of the device counts, packed (and divided by the first pending
+        divisor) on the device; one n(n-1)/2 copy into pinned host memory."""
+        import torch
+        src, n = self._src, self.n
+        m = n * (n - 1) // 2
+        div = float(self._divs[0]) if self._divs else 0.0
+        rest = self._divs[1:] if self._divs else []
+        dt = torch.float64 if div > 0.0 else torch.int64
+        if div > 0.0 and float(self._divs[0]) != self._divs[0]:
+            div = 0.0                                   # a divisor that is not exact in float64: host division
+            rest, dt = self._divs, torch.int64
+        dev = src.device
+        with torch.cuda.device(dev):
+            st = torch.cuda.current_stream(dev)
+            d = torch.empty(max(m, 1), dtype=dt, device=dev)
+            N.check(N.lib().csa_pairs_upper_async(N.ptr(src), n, div, N.ptr(d), ctypes.c_void_p(st.cuda_stream)))
+            h = torch.empty(max(m, 1), dtype=dt, pin_memory=True)
+            h.copy_(d, non_blocking=True)
+            st.synchronize()
+        u = h.numpy()[:m]
+        for dv in rest:
+            u = u / dv
+        return u
 
     @property
-    def _m(self):
-        if self._mat is None:
-            m = self._src.cpu().numpy().reshape(self.n, self.n)
-            for d in self._divs:
-                m = m / d
-            self._mat, self._src, self._divs = m, None, []
-        return self._mat
+    def _u(self):
+        if self._uv is None:
+            if isinstance(self._src, np.ndarray):
+                u = self._src[np.triu_indices(self.n, 1)]
+                for d in self._divs:
+                    u = u / d
+            else:
+                u = self._materialise_device()
+            self._uv, self._src, self._divs = u, None, []
+        return self._uv
 
-    @_m.setter
-    def _m(self, value):
-        self._mat, self._src, self._divs = value, None, []
+    @_u.setter
+    def _u(self, value):
+        self._uv, self._src, self._divs = value, None, []
+
+    def _index(self, i, j):
+        return i * (self.n - 1) - i * (i - 1) // 2 + (j - i - 1)
 
     # dict-compatible accessors -----------------------------------------------------------
     def _key(self, key):
@@ -87,50 +120,59 @@ class PairHistogram:
 
     def __getitem__(self, key):
         i, j = self._key(key)
-        v = self._m[i, j]
-        return v.item()
+        return self._u[self._index(i, j)].item()
+
+    def _writable(self, as_float):
+        u = self._u
+        if as_float and u.dtype.kind != "f":
+            u = u.astype(np.float64)
+        elif not u.flags.writeable or u.base is not None:
+            u = u.copy()
+        self._u = u
+        return u
 
     def __setitem__(self, key, value):
         i, j = self._key(key)
         self._counts = self._S = None
-        if isinstance(value, float) and self._m.dtype.kind != "f":
-            self._m = self._m.astype(np.float64)
-        self._m[i, j] = value
+        self._writable(isinstance(value, float))[self._index(i, j)] = value
 
     def turn_into_probabilities_by_dividing_all_elements_by_given_number(self, num):
-        if self._mat is None:
+        if self._uv is None:
             self._divs.append(num)
         else:
-            self._m = self._m / num
+            self._u = self._uv / num
         self._counts = self._S = None
 
     def add_portfolio_of_panels_to_histogram(self, portfolio, probabilities):
         self._counts = self._S = None
         for panel, pob in zip(portfolio, probabilities):
             idx = np.asarray(sorted(panel), np.int64)
-            if isinstance(pob, float) and self._m.dtype.kind != "f":
-                self._m = self._m.astype(np.float64)
+            u = self._writable(isinstance(pob, float))
             ii, jj = np.triu_indices(len(idx), 1)
-            np.add.at(self._m, (idx[ii], idx[jj]), pob)
+            np.add.at(u, self._index(idx[ii], idx[jj]), pob)
 
     def upper(self):
-        """Values of all pairs i < j in the reference's key order (row-major)."""
-        return self._m[np.triu_indices(self.n, 1)]
+        """Values of all pairs i < j in the reference's key order (row-major); read-only."""
+        u = self._u.view()
+        u.flags.writeable = False
+        return u
 
     def get_dict(self):
         iu = np.triu_indices(self.n, 1)
-        vals = self._m[iu].tolist()
+        vals = self._u.tolist()
         return dict(zip(zip(iu[0].tolist(), iu[1].tolist()), vals))
 
     def __len__(self):
         return self.n * (self.n - 1) // 2
 
     def __getstate__(self):
-        return {"n": self.n, "m": self._m}
+        return {"n": self.n, "u": np.ascontiguousarray(self._u)}
 
     def __setstate__(self, st):
         self.n = st["n"]
-        self._src, self._divs, self._mat = None, [], st["m"]
+        self._src, self._divs, self._uv = None, [], st.get("u")
+        if self._uv is None:                     # round-4 pickles held the n*n matrix
+            self._uv = np.asarray(st["m"])[np.triu_indices(self.n, 1)]
         self._counts = self._S = None
 
 
@@ -153,15 +195,16 @@ class PanelSet:
         return self._count
 
     _where = "panels were not kept; only len() is available"
-    # a sharded run (distributed.ShardGather): the collective that brings the ranks' distinct panels
-    # to rank 0, made on first need; _root: this process is rank 0
+    # a sharded run gathered lazily (distributed.ShardGather): the collective that brings the ranks'
+    # distinct panels to rank 0, made only by an explicit gather() on every rank; _root: this
+    # process is rank 0
     _source = None
     _root = True
 
     def gather(self):
-        """Collective for a sharded run's found_panels (every rank calls it, or iterates / pickles):
-        the ranks' exact local distinct panels go to rank 0.  Called implicitly by iteration, `in`,
-        rows() and pickling; a no-op after the first time and for single-process results."""
+        """The collective of a lazily gathered sharded run's found_panels (every rank calls it, in the
+        same order as the runs): the ranks' exact local distinct panels go to rank 0.  A no-op after
+        the first time and for results that were gathered already or never sharded."""
         if self._source is not None:
             src, self._source = self._source, None
             p = src()
@@ -169,7 +212,10 @@ class PanelSet:
                 self._packed = p
 
     def _materialise(self):
-        self.gather()
+        if self._source is not None:
+            # never an implicit collective: a rank that iterates alone would wait in it forever
+            raise RuntimeError("found_panels of a sharded run were not gathered yet: call "
+                               "found_panels.gather() on every rank first (len() is already global)")
         if self._set is None:
             if self._packed is None:
                 raise RuntimeError(self._where)
@@ -196,7 +242,8 @@ class PanelSet:
         """The distinct panels as a host uint64[u, W] array (sorted rows), or None when the panels
         were not kept (or on a rank other than 0 of a sharded run).  Device panels are copied to the
         host here."""
-        self.gather()
+        if self._source is not None:
+            self._materialise()              # raises: not gathered yet
         W = (self._n + 63) // 64
         if self._packed is None:
             if self._set is None:
@@ -218,6 +265,8 @@ class PanelSet:
     # data -- the distinct panels as packed rows (or the materialised set) -- so the pickle loads
     # on a machine without a GPU
     def __getstate__(self):
+        if self._source is not None:
+            self._materialise()              # raises: not gathered yet
         st = {"count": self._count, "n": self._n, "ids": self._ids}
         if self._set is not None:
             st["set"] = self._set
@@ -290,8 +339,16 @@ LAST_RUN_STATS = None
 
 def reset_draw_stats(enc, stream=None):
     """Zero the instance's draw statistics before a batch: ordered on ``stream`` (a torch stream the
-    batch's draws run on; no host wait), or, without one, after the instance's own streams are idle
-    (csa_instance_draw_stats_reset) -- never a device-wide synchronisation."""
+    batch's draws run on; no host wait), or, without one, after the instance's own streams and the
+    streams of the encoding's cached DevicePipeline (its draw stream included: draws a caller
+    enqueued there may still be counting) are idle (csa_instance_draw_stats_reset) -- never a
+    device-wide synchronisation.  A caller that drew on streams of its own (bench.py)
+    synchronises them first or passes the stream."""
+    if stream is None:
+        pipe = getattr(enc, "_pipe", None)
+        for st in (getattr(pipe, "draw_stream", None), getattr(pipe, "stream", None)):
+            if st is not None:
+                st.synchronize()
     N.check(N.lib().csa_instance_draw_stats_reset(enc.handle, ctypes.c_void_p(stream.cuda_stream)
                                                   if stream is not None else None))
 
@@ -337,6 +394,22 @@ def legacy_sample_raw(enc, k, iterations, random_seed, panel_begin=0, want_pairs
     return LegacyRaw(counts, pairs, int(unique[0]), panels, attempts, draw_stats(enc))
 
 
+def cached_pipeline(enc, k, chunk):
+    """The encoding's DevicePipeline for draws of at most ``chunk`` panels per launch on the current
+    device (picks / XT / pair scratch sized to one chunk, reused across calls; no n*n pair matrix of
+    its own -- callers pass a fresh one per call).  Rebuilt when k, the device or a larger chunk
+    asks for it."""
+    import torch
+    from .device import DevicePipeline
+    pipe = getattr(enc, "_pipe", None)
+    dev = torch.device("cuda", torch.cuda.current_device())
+    if pipe is None or pipe.max_panels < int(chunk) or pipe.k != int(k) or pipe.device != dev:
+        enc._pipe = None                      # release the old buffers before allocating new ones
+        pipe = enc._pipe = DevicePipeline(enc, k, int(chunk), want_pairs=True, want_unique=True, pairs_buffer=False,
+                                          device=dev)
+    return pipe
+
+
 def legacy_sample_device(enc, k, S, random_seed, keep_panels=True, chunk=1 << 20, host_panels=None,
                          host_stats=None):
     """One legacy_probabilities batch on the device through a DevicePipeline cached with the
@@ -348,14 +421,10 @@ def legacy_sample_device(enc, k, S, random_seed, keep_panels=True, chunk=1 << 20
     replaces the device draw; the counting, pairs and distinct count still run on the device
     (``host_stats``: that draw's statistics)."""
     import torch
-    from .device import DevicePipeline
     from .distributed import HashTable
     S = int(S)
-    pipe = getattr(enc, "_pipe", None)
     C = max(1, min(S, int(chunk)))
-    if pipe is None or pipe.max_panels < C or pipe.k != int(k):
-        # want_pairs for the XT / pair scratch; the n*n pair matrix is a fresh tensor per call
-        pipe = enc._pipe = DevicePipeline(enc, k, C, want_pairs=True, want_unique=True, pairs_buffer=False)
+    pipe = cached_pipeline(enc, k, C)
     W = enc.W
     dev = pipe.device
     with torch.cuda.device(dev), torch.cuda.stream(pipe.stream):
@@ -392,10 +461,24 @@ def legacy_sample_device(enc, k, S, random_seed, keep_panels=True, chunk=1 << 20
             N.check(N.lib().csa_unique_async(N.ptr(hashes), N.ptr(panels), S, W, N.ptr(table.table), table.slots,
                                              N.ptr(table.count), N.ptr(pipe.status),
                                              ctypes.c_void_p(pipe.stream.cuda_stream)))
-            counts = pipe.counts.cpu().numpy()       # synchronises the stream
-            unique = int(table.count.item())
-            pipe.check_status()
-            stats = draw_stats(enc) if host_panels is None else host_stats
+            # counts, distinct count, draw statistics and status in ONE copy: the call's one host wait
+            parts = [pipe.counts, table.count]
+            if host_panels is None:
+                st_d = torch.zeros(3, dtype=torch.int64, device=dev)
+                N.check(N.lib().csa_instance_draw_stats_async(enc.handle, N.ptr(st_d),
+                                                              ctypes.c_void_p(pipe.stream.cuda_stream)))
+                parts.append(st_d)
+            h = torch.cat(parts + [pipe.status.to(torch.int64)]).cpu().numpy()
+            n_ = enc.n
+            status = (h[-4:] & 0xFFFFFFFF).astype(np.uint32)
+            if status[0]:
+                rc = N.lib().csa_status_decode(N.ptr(status))
+                if rc == N.CSA_E_NO_CANDIDATE:
+                    raise KeyError("")       # legacy.py:188
+                N.check(rc)
+            counts = h[:n_].copy()
+            unique = int(h[n_])
+            stats = dict(zip(STAT_KEYS, (int(x) for x in h[n_ + 1:n_ + 4]))) if host_panels is None else host_stats
         finally:
             pipe.panels, pipe.hashes, pipe.pairs = own_p, own_h, own_pairs
     return LegacyRaw(counts, pairs.view(enc.n, enc.n), unique, panels[: S * W] if keep_panels else None, None,
@@ -404,7 +487,7 @@ def legacy_sample_device(enc, k, S, random_seed, keep_panels=True, chunk=1 << 20
 
 def legacy_probabilities(instance: Instance, iterations: int, random_seed: int,
                          keep_panels: bool = True, rng: str = None,
-                         devices=None) -> Tuple[ProbAllocation, PanelSet, PairHistogram]:
+                         devices=None, gather: str = "eager") -> Tuple[ProbAllocation, PanelSet, PairHistogram]:
     """analysis.py:162-191 on the GPU.
 
     Returns ``({agent_id: count/S}, found_panels, pair_histogram)`` with the
@@ -420,6 +503,10 @@ def legacy_probabilities(instance: Instance, iterations: int, random_seed: int,
 
     ``devices`` (Philox mode, one process): shard the panels over these HIP
     devices through csa_legacy_sample_devices instead of torch.distributed.
+
+    ``gather`` (sharded runs only): "eager" gathers found_panels to rank 0 inside the call, "lazy"
+    leaves them on the ranks until every rank calls ``found_panels.gather()`` (see
+    ``distributed.legacy_probabilities_distributed``).
     """
     from . import distributed as D
     mode = rng or _legacy.RNG_MODE
@@ -438,7 +525,8 @@ def legacy_probabilities(instance: Instance, iterations: int, random_seed: int,
                                    host_stats=dict(zip(STAT_KEYS, (int(x) for x in st))))
         return finish(instance, enc, raw, S)
     if D.world_size() > 1:
-        return D.legacy_probabilities_distributed(instance, iterations, random_seed, keep_panels=keep_panels)
+        return D.legacy_probabilities_distributed(instance, iterations, random_seed, keep_panels=keep_panels,
+                                                  gather=gather)
     seed(random_seed)
     enc.check_quotas(instance.k)
     STREAM.take_panels(S)

@@ -1679,6 +1679,23 @@ __global__ __launch_bounds__(256) void pairs_unpack_kernel(const int32_t *__rest
     for (int j = i + (int)threadIdx.x; j < n; j += blockDim.x) pairs[(uint64_t)i * n + j] = packed[off + (j - i)];
 }
 
+// PairHistogram materialisation (analysis.py:86-98): the STRICT upper triangle (i < j, the reference's
+// key order, analysis.py:70) of the n x n int64 pair counts packed row-major -- as int64 counts, or as
+// float64 count / divisor (IEEE division, correctly rounded: the value Python's int / int gives, as
+// turn_into_probabilities_by_dividing_all_elements_by_given_number divides).  Row i starts at
+// i (n - 1) - i (i - 1) / 2.  One workgroup per row, coalesced reads and writes; HBM-bound.
+template <bool DIV>
+__global__ __launch_bounds__(256) void pairs_upper_kernel(const int64_t *__restrict__ pairs, int n, double divisor,
+                                                          void *__restrict__ out) {
+    const int i = blockIdx.x;
+    const uint64_t off = (uint64_t)i * (n - 1) - (uint64_t)i * (i - 1) / 2 - (uint64_t)(i + 1);
+    const int64_t *row = pairs + (uint64_t)i * n;
+    for (int j = i + 1 + (int)threadIdx.x; j < n; j += blockDim.x) {
+        if constexpr (DIV) static_cast<double *>(out)[off + j] = (double)row[j] / divisor;
+        else static_cast<int64_t *>(out)[off + j] = row[j];
+    }
+}
+
 // Small-range variant (n_bins <= kHistLdsBins): per-workgroup LDS histogram over a stride of
 // rows (u32 LDS atomics), flushed with one global atomic per non-zero bin -- few distinct values
 // (n = 8192, S = 2e4: ~700 bins for 33.5 M pairs) would otherwise serialise on global atomics.
@@ -1854,6 +1871,9 @@ const void *solo_fn(int fn_, int wn) {
     switch (fn_) {
         case 8: return solo_fn_w<8>(wn);
         case 16: return solo_fn_w<16>(wn);
+#ifdef CSA_SOLO32
+        case 32: return solo_fn_w<32>(wn);
+#endif
         default: return nullptr;
     }
 }
@@ -1918,6 +1938,9 @@ int pick_draw_config(const csa_instance *I, bool general, DrawConfig &c) {
     if (const char *e = getenv("CSA_DRAW_KERNEL")) {
         // the register kernels are built for the shapes they win on only (solo F <= 16, lane F > 16)
         if (!general && !strcmp(e, "solo") && solo_ok) choice = 1;
+#ifdef CSA_SOLO32
+        else if (!general && !strcmp(e, "solo") && lane_ok) choice = 1;
+#endif
         else if (!general && !strcmp(e, "lane") && lane_ok && !solo_ok) choice = 2;
         else if (!general && !strcmp(e, "wide") && wide_ok) choice = 8;
         else if (!general && !strcmp(e, "16") && g16_ok) choice = 16;
@@ -2136,6 +2159,29 @@ int launch_draw(const csa_instance *I, int32_t k, uint64_t seed, uint64_t panel_
         HIPCHK(hipEventRecord(M->picks_done, stream));
         M->picks_pending = true;
     }
+    return CSA_OK;
+}
+
+// panels one full round of the batch draw's resident workgroups covers (CUs x resident workgroups
+// per CU x panels per workgroup): a launch of a multiple of it ends without a part-empty last round
+int draw_round_panels(const csa_instance *I, int32_t k, uint64_t *out) {
+    *out = 0;
+    int rc = check_k(I, k);
+    if (rc) return rc;
+    DrawConfig cfg;
+    if ((rc = pick_draw_config(I, false, cfg))) return rc;
+    const int threads = cfg.lane   ? kLaneThreads
+                        : cfg.solo ? kSoloThreads
+                        : cfg.wide ? kWideThreads
+                                   : draw_threads(cfg.FPL, cfg.WPL);
+    const size_t lds = cfg.lane   ? lane_lds_bytes(cfg.FPL, cfg.WPL, I->n)
+                       : cfg.solo ? solo_lds_bytes(cfg.FPL, cfg.WPL, I->n)
+                       : cfg.wide ? wide_lds_bytes(cfg.G, cfg.FPL, cfg.WPL)
+                                  : draw_lds_bytes(cfg.G, cfg.FPL, cfg.WPL, I->W, k, threads / cfg.G);
+    int per_cu = 0, cus = 0;
+    HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, cfg.fn, threads, lds));
+    HIPCHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, I->device));
+    *out = (uint64_t)std::max(per_cu, 1) * (uint64_t)std::max(cus, 1) * (uint64_t)(threads / cfg.G);
     return CSA_OK;
 }
 
@@ -2396,6 +2442,27 @@ int csa_instance_draw_stats(csa_instance *I, int32_t reset, uint64_t *out) {
     return CSA_OK;
 }
 
+// d_out[0..2] = attempts, SelectionErrors, rejections of the instance's draws so far (not its
+// replicas'), written on `stream` -- no host wait (the sharded legacy_probabilities folds them into
+// its one host read)
+__global__ void draw_stats_copy_kernel(const unsigned long long *__restrict__ st, uint64_t drawn,
+                                       uint64_t *__restrict__ out) {
+    if (threadIdx.x == 0) {
+        out[0] = drawn + st[0] + st[1];
+        out[1] = st[0];
+        out[2] = st[1];
+    }
+}
+
+int csa_instance_draw_stats_async(csa_instance *I, uint64_t *d_out, void *stream) {
+    if (!I || !d_out) return fail(CSA_E_INVALID, "draw_stats_async: bad arguments");
+    ScopedDevice sd(I->device);
+    hipLaunchKernelGGL(draw_stats_copy_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, I->d_stats,
+                       (uint64_t)I->panels_drawn, d_out);
+    HIPCHK(hipGetLastError());
+    return CSA_OK;
+}
+
 int csa_instance_draw_stats_reset(csa_instance *I, void *stream) {
     if (!I) return fail(CSA_E_INVALID, "draw_stats_reset: null instance");
     std::vector<csa_instance *> all{I};
@@ -2507,6 +2574,19 @@ int csa_pairs_pack_async(const int64_t *d_pairs, int32_t n, int32_t *d_packed, v
     return CSA_OK;
 }
 
+int csa_pairs_upper_async(const int64_t *d_pairs, int32_t n, double divisor, void *d_out, void *stream) {
+    if (n < 0 || (n > 1 && (!d_pairs || !d_out)) || divisor < 0.0) return fail(CSA_E_INVALID, "pairs upper: bad arguments");
+    if (n < 2) return CSA_OK;
+    if (divisor > 0.0)
+        hipLaunchKernelGGL(pairs_upper_kernel<true>, dim3((unsigned)(n - 1)), dim3(256), 0, (hipStream_t)stream, d_pairs,
+                           n, divisor, d_out);
+    else
+        hipLaunchKernelGGL(pairs_upper_kernel<false>, dim3((unsigned)(n - 1)), dim3(256), 0, (hipStream_t)stream, d_pairs,
+                           n, 0.0, d_out);
+    HIPCHK(hipGetLastError());
+    return CSA_OK;
+}
+
 int csa_pairs_unpack_async(const int32_t *d_packed, int32_t n, int64_t *d_pairs, void *stream) {
     if (n <= 0 || !d_pairs || !d_packed) return fail(CSA_E_INVALID, "pairs unpack: bad arguments");
     hipLaunchKernelGGL(pairs_unpack_kernel, dim3((unsigned)n), dim3(256), 0, (hipStream_t)stream, d_packed, n, d_pairs);
@@ -2551,6 +2631,12 @@ int csa_status_decode(const uint32_t *h) {
         default:
             return fail((int)h[0], "device status %u at panel %llu", h[0], (unsigned long long)panel);
     }
+}
+
+int csa_draw_round_panels(const csa_instance *I, int32_t k, uint64_t *out) {
+    if (!I || !out) return fail(CSA_E_INVALID, "draw_round_panels: bad arguments");
+    ScopedDevice sd(I->device);
+    return draw_round_panels(I, k, out);
 }
 
 int csa_draw_async(const csa_instance *I, int32_t k, uint64_t seed, uint64_t panel_begin, uint64_t n_panels,

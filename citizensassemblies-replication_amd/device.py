@@ -28,6 +28,28 @@ def _stream_ptr(stream):
     return ctypes.c_void_p(stream.cuda_stream) if stream is not None else None
 
 
+def chunk_plan(S, C, R):
+    """Chunk sizes (summing to S, each <= C) for DevicePipeline.draw_count_chunks.  R > 0 is the
+    draw's round (csa_draw_round_panels): every chunk but the last is a whole number of rounds, so
+    no launch but the last ends in a part-empty round of waves, and the last two are one round and
+    the remainder, so the counting of the big chunk runs beside two short draws and only the
+    remainder's counting follows the last draw.  R = 0: equal cuts of at most C (flat)."""
+    S, C = int(S), max(1, int(C))
+    if S <= 0:
+        return []
+    if R <= 0 or S <= R or R > C:
+        return [min(C, S - off) for off in range(0, S, C)]
+    tail = S - R * ((S - 1) // R)                 # in (0, R]
+    head = S - tail - R                           # whole rounds before the last full one
+    Cr = (C // R) * R
+    sizes = []
+    while head > 0:
+        c = min(Cr, head)
+        sizes.append(c)
+        head -= c
+    return sizes + [R, tail]
+
+
 class DevicePipeline:
     def __init__(self, enc, k, max_panels, want_pairs=True, want_unique=True, want_attempts=False,
                  device=None, stream=None, pair_engine=N.CSA_PAIR_FP4, pairs_buffer=True):
@@ -141,6 +163,17 @@ class DevicePipeline:
                                          N.ptr(self.table), self.slots, N.ptr(self.unique), N.ptr(self.status),
                                          _stream_ptr(self.stream)))
 
+    def round_panels(self):
+        """Panels one full round of the batch draw's resident workgroups covers on this device
+        (csa_draw_round_panels; 131072 for the two-lane kernel on 256 CUs)."""
+        rp = getattr(self, "_round", None)
+        if rp is None:
+            import numpy as np
+            out = np.zeros(1, np.uint64)
+            N.check(N.lib().csa_draw_round_panels(self.enc.handle, self.k, N.ptr(out)))
+            rp = self._round = max(1, int(out[0]))
+        return rp
+
     def draw_count_chunks(self, seed, panel_begin, S, panels, hashes, chunk, overwrite_pairs=False):
         """Draw S panels (global indices panel_begin ..) into ``panels`` / ``hashes`` (tensors of the
         whole batch) and accumulate their counts and pairs, in chunks of at most ``chunk`` panels
@@ -149,9 +182,17 @@ class DevicePipeline:
         beside the draw of chunk c + 1 (bench.py's pipeline).  The first chunk stores its pair counts
         with ``overwrite_pairs``; later chunks add theirs.  Ordered after everything already on the
         pipeline stream; on return the pipeline stream is ordered after every draw."""
+        import os
         import torch
         S, C, W = int(S), max(1, min(int(chunk), self.max_panels)), self.enc.W
-        chunks = [(off, min(C, S - off)) for off in range(0, S, C)]
+        # flat cuts by default: the round-aligned plan (CSA_CHUNK_PLAN=round) measured slower end to end
+        # (sf_e 10^6 panels 4.59 vs 4.41 ms, example_large_200 1.25e6 5.02 vs 4.99, synthetic8192 10^6
+        # 33.0 vs 32.2; profiles/r05_api_chunk_plan.txt): the big chunk's counting slows the short draws
+        sizes = chunk_plan(S, C, self.round_panels() if os.environ.get("CSA_CHUNK_PLAN") == "round" else 0)
+        chunks, off = [], 0
+        for ln in sizes:
+            chunks.append((off, ln))
+            off += ln
         st = getattr(self, "draw_stream", None)
         if st is None:
             st = self.draw_stream = torch.cuda.Stream(self.device)

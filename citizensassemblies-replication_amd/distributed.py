@@ -232,9 +232,14 @@ class PanelExchange:
         per = 24 if self.redraw is not None else 16 + 8 * self.W
         return self.world * self.cap * per + 8 * self.world
 
-    def run(self, hashes, panels, n, status=None, stream=None, panel_begin=0):
+    def run(self, hashes, panels, n, status=None, stream=None, panel_begin=0, redraw=None):
+        """``redraw`` overrides the constructor's (instance, k, seed, max_attempts) for this run (a
+        cached exchange serves calls with different seeds); the form -- keys or bitmasks -- is the
+        constructor's."""
         import torch
         n = int(n)
+        if redraw is not None and self.redraw is not None:
+            self.redraw = redraw
         assert n <= self.n_local
         if not hashes.is_cuda:
             import torch.distributed as dist
@@ -401,21 +406,40 @@ def local_distinct_rows(hashes, panels, n, W, status=None, stream=None):
 GATHER_CHUNK_BYTES = 256 << 20   # rows per point-to-point message of the found_panels gather
 
 
-def gather_distinct_to_root(hashes, panels, n, W, status=None, stream=None, chunk_bytes=None):
+def _check_run_id(run_id, dev):
+    """Every rank of a gather must be gathering the same run (the ranks' n-th sharded call): an
+    all_reduce(MAX) of (id, -id) equals (id, -id) on every rank iff all ids agree; else every rank
+    raises (consistently: they all see the same reduced values), instead of rank 0 receiving
+    another run's panels."""
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([int(run_id), -int(run_id)], dtype=torch.int64, device=dev)
+    _all_reduce(t, op=dist.ReduceOp.MAX)
+    hi, lo = (int(x) for x in t.cpu().tolist())
+    if hi != int(run_id) or -lo != int(run_id):
+        raise RuntimeError("found_panels gather: the ranks are gathering different runs (run ids %d..%d; this "
+                           "rank: %d) -- gather() the sharded results in the same order on every rank"
+                           % (-lo, hi, int(run_id)))
+
+
+def gather_distinct_to_root(hashes, panels, n, W, status=None, stream=None, chunk_bytes=None, run_id=None):
     """found_panels of a sharded run, on rank 0 only (a collective: every rank calls it): every rank
     reduces its shard to its exact local distinct panels; one all_reduce tells rank 0 every rank's
     count, rank 0 allocates ONE host array for all of them and receives each rank's rows straight
     into its slice, in messages of at most ``chunk_bytes`` (no concatenated copy; over RCCL each
     message lands in a device buffer of that size first), so no rank ever holds more than its own
-    panels on its device.  Returns uint64[m, W] on rank 0 (rows of all ranks; a panel drawn on two
-    ranks appears twice and PanelSet deduplicates on iteration), None elsewhere."""
+    panels on its device.  ``run_id``: checked across ranks first (_check_run_id).  Returns
+    uint64[m, W] on rank 0 (rows of all ranks; a panel drawn on two ranks appears twice and
+    PanelSet deduplicates on iteration), None elsewhere."""
     import torch
     import torch.distributed as dist
     world, r = dist.get_world_size(), dist.get_rank()
     W = int(W)
+    host = _host_collectives(hashes) or not hashes.is_cuda
+    dev = torch.device("cpu") if host else hashes.device
+    if run_id is not None:
+        _check_run_id(run_id, dev)
     rows, cnt = local_distinct_rows(hashes, panels, n, W, status, stream)
-    host = _host_collectives(rows) or not rows.is_cuda
-    dev = torch.device("cpu") if host else rows.device
     counts = torch.zeros(world, dtype=torch.int64, device=dev)
     counts[r] = cnt
     _all_reduce(counts)
@@ -446,66 +470,161 @@ def gather_distinct_to_root(hashes, panels, n, W, status=None, stream=None, chun
 
 
 class ShardGather:
-    """found_panels of a sharded run before anyone looked at them: this rank's shard (hashes and
-    panels, kept on its device) and how to gather the ranks' exact local distinct panels to rank 0.
-    Calling it is the collective gather_distinct_to_root (every rank must call it, once); until then
-    legacy_probabilities has sent nothing -- len(found_panels) is the global exact count from the
-    exchange."""
+    """found_panels of a sharded run gathered lazily (gather="lazy"): this rank's shard (hashes and
+    panels, kept on its device until the gather) and how to gather the ranks' exact local distinct
+    panels to rank 0.  Calling it is the collective gather_distinct_to_root (every rank calls it
+    once, through PanelSet.gather(); iteration never calls it implicitly); ``run_id`` ties the
+    gather to its run on every rank."""
 
-    def __init__(self, hashes, panels, n, W, stream=None):
+    def __init__(self, hashes, panels, n, W, stream=None, run_id=None):
         self.hashes, self.panels, self.n, self.W, self.stream = hashes, panels, int(n), int(W), stream
+        self.run_id = run_id
 
     def __call__(self):
-        out = gather_distinct_to_root(self.hashes, self.panels, self.n, self.W, stream=self.stream)
+        out = gather_distinct_to_root(self.hashes, self.panels, self.n, self.W, stream=self.stream,
+                                      run_id=self.run_id)
         self.hashes = self.panels = None
         return out
 
 
-def legacy_probabilities_distributed(instance, iterations, random_seed, keep_panels=True):
+_RUN_SEQ = [0]   # this process's sharded calls, in order (the ranks make them in the same order)
+
+
+def _decode_status(words, reduced_code):
+    """Raise the error of a status block (host uint32[4]); a rank whose own block is clean raises the
+    code another rank reported (KeyError for a missing candidate, legacy.py:188)."""
+    from . import _native as N
+    h = np.asarray(words, np.uint32)
+    if int(h[0]) == 0:
+        h = np.array([reduced_code, 0xFFFFFFFF, 0xFFFFFFFF, 0], np.uint32)
+    rc = N.lib().csa_status_decode(N.ptr(h))
+    if rc == N.CSA_E_NO_CANDIDATE:
+        raise KeyError("")
+    N.check(rc)
+
+
+def _shard_exchange(enc, n_max, world, dev):
+    """The encoding's cached PanelExchange (24-byte keys) for shares of at most n_max panels."""
+    ex = getattr(enc, "_xchg", None)
+    if ex is None or ex.n_local < max(int(n_max), 1) or ex.world != int(world) or ex.device != dev:
+        enc._xchg = None
+        ex = enc._xchg = PanelExchange(n_max, enc.W, world, dev, redraw=(enc.handle, 0, 0, 0))
+    return ex
+
+
+def legacy_probabilities_distributed(instance, iterations, random_seed, keep_panels=True, gather="eager",
+                                     chunk=None, timings=None):
     """analysis.py:162-191 with the panels sharded over the ranks of the default group.  Every rank
-    returns the whole job's alloc, pair histogram and exact distinct-panel count.  With
-    ``keep_panels`` rank 0's ``found_panels`` also iterates like the reference's set: each rank keeps
-    its shard on its device, and the first iteration / `in` / rows() / pickle of found_panels -- a
-    collective, made on every rank (PanelSet.gather) -- sends the ranks' exact local distinct panels
-    to rank 0; on the other ranks it supports len() only.  The draw statistics
-    (analysis.LAST_RUN_STATS) are summed over ranks."""
+    returns the whole job's alloc, pair histogram and exact distinct-panel count.
+
+    Per call (cheap when repeated): the encoding, the device pipeline (picks / XT / pair scratch
+    sized to one ``chunk`` of panels, default 2^20 or CSA_SHARD_CHUNK) and the 24-byte key exchange
+    are cached on the encoding; the share's panels and hashes and the n*n pair matrix are fresh
+    tensors (caching allocator).  Draws, counting, pairs, the draw statistics and every collective
+    are stream-ordered; the host waits once, for one copy of [counts | statistics | distinct count |
+    status].  The pair counts stay on the device behind the returned PairHistogram (packed and
+    divided there when first read).
+
+    found_panels (``keep_panels``):
+      * ``gather="eager"`` (default): the ranks' exact local distinct panels are gathered to rank 0
+        inside this call (a collective every rank is already in); rank 0's set iterates like the
+        reference's, the others support len() only;
+      * ``gather="lazy"``: nothing is sent; each rank keeps its shard on its device until every rank
+        calls ``found_panels.gather()`` (the collective, checked to be the same run on all ranks).
+        Iterating, testing membership, comparing or pickling an un-gathered set raises at once on
+        any rank -- it never enters a collective by itself.
+    The draw statistics (analysis.LAST_RUN_STATS) are summed over ranks.  ``timings`` (a dict) gets
+    the host-side stage times in ms."""
+    import time
     import torch
+    import torch.distributed as dist
     from . import analysis as A
-    from .device import DevicePipeline
-    from .instance import encode
+    from . import _native as N
+    if gather not in ("eager", "lazy"):
+        raise ValueError("gather must be 'eager' or 'lazy'")
+    t0 = time.perf_counter()
     world, r = world_size(), rank()
     S = int(iterations)
     A.seed(random_seed)
     A.STREAM.take_panels(S)
-    enc = encode(instance.categories, instance.agents)
-    enc.check_quotas(instance.k)
+    enc = A.encode_cached(instance.categories, instance.agents)
+    k = int(instance.k)
+    enc.check_quotas(k)
     begin, end = shard_range(S, world, r)
     local = end - begin
+    n_max = shard_range(S, world, 0)[1]          # rank 0 holds the largest share
+    _RUN_SEQ[0] += 1
+    run_id = _RUN_SEQ[0]
     # one process per GPU (LOCAL_RANK); the modulo lets rehearsals put several ranks on one device
     torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", r)) % max(torch.cuda.device_count(), 1))
-    pipe = DevicePipeline(enc, instance.k, max(local, 1), want_pairs=True, want_unique=True)
-    pipe.reset()
-    A.reset_draw_stats(enc, pipe.stream)
-    if local:
-        # the shard in chunks (default 2^20 panels; CSA_SHARD_CHUNK), each chunk's counting and pairs
-        # beside the next chunk's draw
-        pipe.draw_count_chunks(random_seed, begin, local, pipe.panels, pipe.hashes,
-                               int(os.environ.get("CSA_SHARD_CHUNK", 1 << 20)))
-    _raise_together(pipe.status, pipe.stream)
-    counts, pairs, u = combine(pipe.counts, pipe.pairs, pipe.hashes[: 2 * local], pipe.panels[: local * enc.W],
-                               enc.W, pair_bound=S, status=pipe.status, redraw=(enc.handle, instance.k, random_seed, 0),
-                               panel_begin=begin)
-    _raise_together(pipe.status, pipe.stream)
-    stats = torch.tensor(list(A.draw_stats(enc).values()), dtype=torch.int64, device=pipe.counts.device)
-    _all_reduce(stats)
-    raw = A.LegacyRaw(counts.cpu().numpy(), pairs.cpu().numpy().reshape(enc.n, enc.n), int(u.item()), None, None,
-                      dict(zip(A.STAT_KEYS, (int(x) for x in stats.cpu().tolist()))))
+    dev = torch.device("cuda", torch.cuda.current_device())
+    C = max(1, min(max(local, 1), int(chunk or os.environ.get("CSA_SHARD_CHUNK", 1 << 20))))
+    pipe = A.cached_pipeline(enc, k, C)
+    # (CSA_FORCE_EXCHANGE=1: the key exchange even for one rank -- tests of its collectives on one GPU)
+    ex = _shard_exchange(enc, n_max, world, dev) if world > 1 or os.environ.get("CSA_FORCE_EXCHANGE") == "1" else None
+    W, n = enc.W, enc.n
+    L = N.lib()
+    st = pipe.stream
+    sp = ctypes.c_void_p(st.cuda_stream)
+    t1 = time.perf_counter()
+    with torch.cuda.device(dev), torch.cuda.stream(st):
+        panels = torch.empty(max(local * W, 1), dtype=torch.int64, device=dev)
+        hashes = torch.empty(max(2 * local, 2), dtype=torch.int64, device=dev)
+        pairs = torch.empty(n * n, dtype=torch.int64, device=dev)
+        # [counts (n) | attempts, SelectionErrors, rejections | distinct count]: one all_reduce(SUM)
+        acc = torch.zeros(n + 4, dtype=torch.int64, device=dev)
+        pipe.reset(pairs=False)
+        A.reset_draw_stats(enc, st)
+        own_counts, own_pairs = pipe.counts, pipe.pairs
+        pipe.counts, pipe.pairs = acc[:n], pairs
+        try:
+            if local:
+                pipe.draw_count_chunks(random_seed, begin, local, panels, hashes, C, overwrite_pairs=True)
+            else:
+                pairs.zero_()
+        finally:
+            pipe.counts, pipe.pairs = own_counts, own_pairs
+        # this shard's draw statistics, before the exchange's re-draws (device, no host wait)
+        N.check(L.csa_instance_draw_stats_async(enc.handle, N.ptr(acc[n:n + 3]), sp))
+        _all_reduce_pairs(pairs, S, st)
+        if ex is not None:
+            u = ex.run(hashes, panels, local, status=pipe.status, stream=st, panel_begin=begin,
+                       redraw=(enc.handle, k, random_seed, 0))
+        else:           # one rank owns every panel: the exact local count, no exchange
+            table = getattr(enc, "_table", None)
+            if table is None:
+                table = enc._table = HashTable(local, dev)
+            table.ensure(local)
+            table.count.zero_()
+            N.check(L.csa_unique_async(N.ptr(hashes), N.ptr(panels), local, W, N.ptr(table.table), table.slots,
+                                       N.ptr(table.count), N.ptr(pipe.status), sp))
+            u = table.count
+        acc[n + 3:].copy_(u)
+        _all_reduce(acc)
+        code = pipe.status[:1].to(torch.int64)
+        _all_reduce(code, op=dist.ReduceOp.MAX)
+        tail = torch.cat([code, pipe.status.to(torch.int64)])
+        host = torch.cat([acc, tail]).cpu()          # the call's one host wait
+    t2 = time.perf_counter()
+    h = host.numpy()
+    if int(h[n + 4]):
+        _decode_status((h[n + 5:n + 9] & 0xFFFFFFFF).astype(np.uint32), int(h[n + 4]))
+    counts = h[:n].copy()
+    stats = dict(zip(A.STAT_KEYS, (int(x) for x in h[n:n + 3])))
+    raw = A.LegacyRaw(counts, pairs.view(n, n), int(h[n + 3]), None, None, stats)
     out = A.finish(instance, enc, raw, S)
     if keep_panels:
-        # lazy: the shard stays on this rank's device; the first iteration / `in` / rows() / pickle of
-        # found_panels (a collective -- every rank makes it) gathers the distinct panels to rank 0
-        out[1]._source = ShardGather(pipe.hashes[: 2 * local], pipe.panels[: local * enc.W], local, enc.W,
-                                     pipe.stream)
+        sg = ShardGather(hashes[: 2 * local], panels[: local * W], local, W, st, run_id=run_id)
         out[1]._root = r == 0
         out[1]._where = "found_panels of a sharded run iterate on rank 0 only (len() is global)"
+        if gather == "eager":
+            p = sg()
+            if r == 0:
+                out[1]._packed = p
+        else:
+            out[1]._source = sg
+    if timings is not None:
+        t3 = time.perf_counter()
+        timings.update(setup_ms=(t1 - t0) * 1e3, device_ms=(t2 - t1) * 1e3, finish_ms=(t3 - t2) * 1e3,
+                       total_ms=(t3 - t0) * 1e3)
     return out

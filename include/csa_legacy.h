@@ -90,6 +90,10 @@ int csa_instance_draw_stats(csa_instance *inst, int32_t reset, uint64_t *out);
  * after the instance's own streams (csa_legacy_sample's pipeline) are idle.  Other streams of the
  * device are never waited for. */
 int csa_instance_draw_stats_reset(csa_instance *inst, void *stream);
+/* The same totals as csa_instance_draw_stats (this instance only, not csa_legacy_sample_devices'
+ * replicas) written to device memory d_out[0..2] by a kernel on `stream`: no host wait, so a
+ * caller orders it after its draws and reads it together with its other results. */
+int csa_instance_draw_stats_async(csa_instance *inst, uint64_t *d_out, void *stream);
 
 /* check_same_address (legacy.py:78-99, 103-113): addr_next (n int32) links the agents that share
  * an address (the check_same_address_columns values) into rings, agent order: addr_next[p] = the
@@ -186,9 +190,19 @@ int csa_legacy_draw_mt(int32_t n, int32_t C, int32_t F, const int32_t *person_fe
  * result) which the caller zeroes before the first launch and decodes with
  * csa_status_decode after synchronising. */
 
-/* Draw kernel: one panel per wavefront, LDS-resident feature bitmasks.
- * d_panels: n_panels*W (required); d_hashes: 2*n_panels 128-bit panel hashes
+/* Batch draw (analysis.py:141-159 per panel).  The instance's shape picks the kernel: a panel's
+ * state (per-feature need / remaining keys and the remaining-pool bitset) lives in REGISTERS, split
+ * over 1 lane (draw_solo_kernel, F <= 16), 2 lanes (draw_lane_kernel, F <= 32, n <= 2048) or 8
+ * lanes (draw_wide_kernel, F <= 64, n <= 8192) of a wavefront, with the feature rows and person
+ * masks in LDS; draw_kernel (16 or 64 lanes per panel) covers every other shape, pick orders and
+ * same-address rings.  d_panels: n_panels*W (required); d_hashes: 2*n_panels 128-bit panel hashes
  * (or NULL); d_attempts: n_panels (or NULL); d_picks: n_panels*k (or NULL). */
+/* Panels one full round of the batch draw's resident workgroups covers on the instance's device
+ * (CUs x resident workgroups per CU x panels per workgroup, for this k): a csa_draw_async launch of
+ * a multiple of it ends without a part-empty last round (callers that cut a batch into chunks use
+ * it to size them).  *out = 0 on error. */
+int csa_draw_round_panels(const csa_instance *inst, int32_t k, uint64_t *out);
+
 int csa_draw_async(const csa_instance *inst, int32_t k, uint64_t seed, uint64_t panel_begin,
                    uint64_t n_panels, uint32_t max_attempts, uint64_t *d_panels,
                    uint64_t *d_hashes, uint32_t *d_attempts, int32_t *d_picks,
@@ -335,6 +349,13 @@ int csa_unique_keys_async(const csa_instance *inst, int32_t k, uint64_t seed, ui
  * < 2^31), and unpack it back (overwriting the upper triangle). */
 int csa_pairs_pack_async(const int64_t *d_pairs, int32_t n, int32_t *d_packed, void *stream);
 int csa_pairs_unpack_async(const int32_t *d_packed, int32_t n, int64_t *d_pairs, void *stream);
+
+/* PairHistogram materialisation (replaces the host-side division and triangle walk of
+ * analysis.py:86-98): the strict upper triangle (i < j, row-major -- the reference's key order,
+ * analysis.py:70) of the n*n int64 pair counts, packed into n(n-1)/2 entries of d_out: float64
+ * count / divisor (IEEE, correctly rounded: Python's int / int) for divisor > 0, int64 counts for
+ * divisor == 0.  Stream-ordered. */
+int csa_pairs_upper_async(const int64_t *d_pairs, int32_t n, double divisor, void *d_out, void *stream);
 
 /* Decode a device status block (host copy of the 4 words) into a CSA_* code
  * and set csa_last_error() accordingly. */

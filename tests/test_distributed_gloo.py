@@ -65,16 +65,24 @@ def _worker(rank, world, port, out_dir, name):
 
     dist.recv = counting_recv
     counts, pairs, u = D.combine(counts, pairs, hashes, ptens, W)
-    # found_panels as legacy_probabilities_distributed returns it: nothing gathered yet, len() global
+    # found_panels as legacy_probabilities_distributed(gather="lazy") returns them: nothing gathered
+    # yet, len() global, and ANY rank that iterates / tests membership / pickles / compares before the
+    # explicit gather() raises at once -- it never enters the collective alone (no hang)
     A = pkg("analysis")
+    import pickle
     found = A.PanelSet(int(u.item()), None, o.n, list(range(o.n)))
-    found._source, found._root = D.ShardGather(hashes, ptens, e - b, W), rank == 0
+    found._source, found._root = D.ShardGather(hashes, ptens, e - b, W, run_id=7), rank == 0
     assert len(found) == int(u.item()) and recvs == []
+    for touch in (lambda: sorted(found), lambda: (1,) in found, lambda: pickle.dumps(found), found.rows,
+                  lambda: found == set()):
+        with pytest.raises(RuntimeError, match="gather"):
+            touch()
+    assert recvs == []
     D.GATHER_CHUNK_BYTES = 8 * W * 7               # 7 rows per message: several messages per rank
+    found.gather()                                 # the explicit collective, on every rank
     if rank == 0:
-        tuples = sorted(found)                     # the collective gather, then the set
+        tuples = sorted(found)
         rows = found.rows()
-        import pickle
         again = pickle.loads(pickle.dumps(found))
         assert sorted(again) == tuples and len(again) == len(found)
         assert all(t in found for t in tuples[:5]) and (-1,) not in found
@@ -84,10 +92,16 @@ def _worker(rank, world, port, out_dir, name):
         np.save(os.path.join(out_dir, "pairs.npy"), pairs.numpy())
         np.save(os.path.join(out_dir, "unique.npy"), np.array([int(u.item())]))
     else:
-        found.gather()                             # this rank's side of the collective
         with pytest.raises(RuntimeError):
             iter(found)
         assert recvs == []
+    # ranks gathering DIFFERENT runs (ids 10 / 11): every rank raises, rank 0 receives nothing
+    other = A.PanelSet(int(u.item()), None, o.n, list(range(o.n)))
+    other._source, other._root = D.ShardGather(hashes, ptens, e - b, W, run_id=10 + rank), rank == 0
+    n_recv = len(recvs)
+    with pytest.raises(RuntimeError, match="different runs"):
+        other.gather()
+    assert len(recvs) == n_recv
     dist.barrier()
     dist.destroy_process_group()
 

@@ -471,6 +471,50 @@ def test_combine_rccl_world1(gpu_available):
     assert int(u.item()) == S      # sf_e_110 at 2e4 panels: all distinct
 
 
+@pytest.mark.parametrize("name,k,S,chunk", [("sf_e_110", 110, 30001, 7000),
+                                            ("couples_panel_from_twenty_people_no_constraints_2", 2, 20000, 0),
+                                            ("synthetic8192_200", 200, 3000, 1000)])
+@pytest.mark.parametrize("force_exchange", ["0", "1"])
+def test_distributed_call_rccl_world1(gpu_available, monkeypatch, name, k, S, chunk, force_exchange):
+    """legacy_probabilities_distributed over a one-rank RCCL group (the product path's own
+    collectives: packed pair all_reduce, the 24-byte key exchange, one all_reduce of counts +
+    statistics + distinct count): equal to legacy_probabilities on one GPU -- alloc, pair values,
+    distinct count, draw statistics, found_panels (eager gather) -- on the first call and on a
+    second call that reuses the cached pipeline and exchange; lazy found_panels fail fast before
+    gather() and equal after it."""
+    import pickle
+    import socket
+    import torch.distributed as dist
+    A = pkg("analysis")
+    Dd = pkg("distributed")
+    if chunk:
+        monkeypatch.setenv("CSA_SHARD_CHUNK", str(chunk))
+    monkeypatch.setenv("CSA_FORCE_EXCHANGE", force_exchange)   # 1: the 24-byte key exchange over RCCL
+    inst = pkg().read_instance(*inst_paths(name), k)
+    alloc, found, hist = A.legacy_probabilities(inst, S, 9)
+    stats = dict(A.LAST_RUN_STATS)
+    want_up, want_found = np.array(hist.upper()), sorted(found)
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    dist.init_process_group("nccl", init_method="tcp://127.0.0.1:%d" % port, rank=0, world_size=1)
+    try:
+        for call in range(2):
+            tm = {}
+            a2, f2, h2 = Dd.legacy_probabilities_distributed(inst, S, 9, timings=tm)
+            assert a2 == alloc and len(f2) == len(found) and A.LAST_RUN_STATS == stats
+            assert np.array_equal(h2.upper(), want_up)
+            assert sorted(f2) == want_found
+            assert tm["total_ms"] > 0
+        a3, f3, h3 = Dd.legacy_probabilities_distributed(inst, S, 9, gather="lazy")
+        with pytest.raises(RuntimeError, match="gather"):
+            pickle.dumps(f3)
+        f3.gather()
+        assert sorted(f3) == want_found and a3 == alloc
+    finally:
+        dist.destroy_process_group()
+
+
 @pytest.mark.parametrize("name,k,S", [("couples_panel_from_twenty_people_no_constraints_2", 2, 300000),
                                       ("example_small_20", 20, 200000), ("sf_e_110", 110, 100000),
                                       ("rejecty_6", 6, 400000)])
@@ -495,7 +539,7 @@ def test_unique_partitioned_matches_oracle(gpu_available, name, k, S):
     assert got["1"] == got["0"] == want
 
 
-def _dist_worker(rank, world, port, out_dir, name, k, S, seed):
+def _dist_worker(rank, world, port, out_dir, name, k, S, seed, mode):
     import os
     import sys
     import torch.distributed as dist
@@ -516,35 +560,48 @@ def _dist_worker(rank, world, port, out_dir, name, k, S, seed):
             return real_recv(tensor, src, *a, **kw)
 
         dist.recv = counting_recv
-        alloc, found, hist = A.legacy_probabilities(inst, S, seed)      # world > 1: sharded
-        assert recvs == []      # found_panels are gathered lazily, not by legacy_probabilities
+        alloc, found, hist = A.legacy_probabilities(inst, S, seed, gather=mode)      # world > 1: sharded
+        if mode == "lazy":
+            assert recvs == []             # nothing sent until the explicit gather
+            with pytest.raises(RuntimeError, match="gather"):
+                sorted(found)              # fails at once on any rank, never waits in a collective
+            with pytest.raises(RuntimeError, match="gather"):
+                pickle.dumps((alloc, found, hist))
+            assert recvs == []
+            found.gather()                 # the collective, every rank
+        assert bool(recvs) == (rank == 0)  # eager: gathered inside the call
         if rank == world - 1:
             np.save(os.path.join(out_dir, "unique_last.npy"), np.array([len(found)]))
         if rank == 0:           # found_panels iterate on rank 0 (the ranks' distinct panels gathered)
             np.save(os.path.join(out_dir, "alloc.npy"), np.array([alloc[i] for i in range(len(alloc))]))
             np.save(os.path.join(out_dir, "upper.npy"), hist.upper())
             np.save(os.path.join(out_dir, "unique.npy"), np.array([len(found)]))
-            tuples = sorted(found)                                     # the collective gather
-            assert recvs
+            tuples = sorted(found)
             assert all(t in found for t in tuples[:3])
             np.save(os.path.join(out_dir, "found.npy"), np.array(tuples))
             with open(os.path.join(out_dir, "result.pkl"), "wb") as f:
                 pickle.dump((alloc, found, hist), f)
         else:
-            pickle.dumps((alloc, found, hist))  # pickling is the other ranks' side of the gather
+            with pytest.raises(RuntimeError):
+                iter(found)                # len() only on the other ranks
+            pickle.dumps((alloc, found, hist))   # holds the count, no collective
         dist.barrier()
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("name,k,S,seed,chunk", [("sf_e_110", 110, 9001, 3, 0), ("sf_e_110", 110, 9001, 4, 1700),
-                                                 ("couples_panel_from_twenty_people_no_constraints_2", 2, 5000, 1, 0)])
-def test_legacy_probabilities_distributed_gloo(gpu_available, tmp_path, monkeypatch, name, k, S, seed, chunk):
+@pytest.mark.parametrize("name,k,S,seed,chunk,mode", [("sf_e_110", 110, 9001, 3, 0, "eager"),
+                                                      ("sf_e_110", 110, 9001, 4, 1700, "lazy"),
+                                                      ("couples_panel_from_twenty_people_no_constraints_2", 2, 5000, 1,
+                                                       0, "eager"),
+                                                      ("couples_panel_from_twenty_people_no_constraints_2", 2, 5000, 2,
+                                                       700, "lazy")])
+def test_legacy_probabilities_distributed_gloo(gpu_available, tmp_path, monkeypatch, name, k, S, seed, chunk, mode):
     """analysis.legacy_probabilities with a 2-rank process group (both ranks on this GPU, gloo:
     RCCL refuses two ranks on one device): the sharded draw (``chunk``: each rank's shard drawn in
     chunks of that many panels, counted beside the next chunk's draw), the exact panel exchange and the
-    found_panels -- gathered to rank 0 only when iterated / pickled (no dist.recv before), `in`,
-    and the pickled tuple -- equal the single-GPU result."""
+    found_panels -- gathered to rank 0 inside the call (eager) or by the explicit gather() (lazy, which
+    fails fast when touched before it) -- `in`, and the pickled tuple equal the single-GPU result."""
     import socket
     import torch.multiprocessing as mp
     A = pkg("analysis")
@@ -553,7 +610,7 @@ def test_legacy_probabilities_distributed_gloo(gpu_available, tmp_path, monkeypa
     with socket.socket() as sk:
         sk.bind(("127.0.0.1", 0))
         port = sk.getsockname()[1]
-    mp.spawn(_dist_worker, args=(2, port, str(tmp_path), name, k, S, seed), nprocs=2, join=True)
+    mp.spawn(_dist_worker, args=(2, port, str(tmp_path), name, k, S, seed, mode), nprocs=2, join=True)
     inst = pkg().read_instance(*inst_paths(name), k)
     alloc, found, hist = A.legacy_probabilities(inst, S, seed)
     assert np.load(tmp_path / "alloc.npy").tolist() == [alloc[i] for i in range(len(alloc))]
@@ -561,6 +618,7 @@ def test_legacy_probabilities_distributed_gloo(gpu_available, tmp_path, monkeypa
     assert int(np.load(tmp_path / "unique.npy")[0]) == len(found)
     assert int(np.load(tmp_path / "unique_last.npy")[0]) == len(found)
     assert np.load(tmp_path / "found.npy").tolist() == [list(p) for p in sorted(found)]
+    assert A.LAST_RUN_STATS["attempts"] >= S
     import pickle
     with open(tmp_path / "result.pkl", "rb") as f:
         _, found_p, _ = pickle.load(f)

@@ -328,3 +328,22 @@ def test_xt_register_transpose_network():
               "xt_dpp<0xB1>"):
         assert c in body, c
     assert re.search(r"c\.r4 = b2 \? 4u : 28u", body)
+
+
+def test_chunk_plan_rounds():
+    """device.chunk_plan: chunks sum to S, stay <= C, are whole rounds except the last (one round
+    before it), and fall back to equal cuts without a round size."""
+    D = pkg("device")
+    R = 131072
+    assert D.chunk_plan(10 ** 6, 1 << 20, R) == [786432, 131072, 82496]
+    assert D.chunk_plan(1250000, 1 << 20, 262144) == [786432, 262144, 201424]
+    assert D.chunk_plan(5, 1 << 20, R) == [5] and D.chunk_plan(0, 10, R) == []
+    assert D.chunk_plan(10, 4, 0) == [4, 4, 2]
+    rng = np.random.default_rng(5)
+    for _ in range(200):
+        S, R = int(rng.integers(1, 10 ** 8)), int(rng.integers(1, 300000))
+        C = int(rng.integers(R, 4 * R + 2))
+        sizes = D.chunk_plan(S, C, R)
+        assert sum(sizes) == S and all(0 < c <= C for c in sizes)
+        if S > R:
+            assert sizes[-2] == R and all(c % R == 0 for c in sizes[:-1])
