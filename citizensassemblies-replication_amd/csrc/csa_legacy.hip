@@ -1750,6 +1750,9 @@ struct csa_instance {
     // need < min - max + 1 (true past max too), so such start states take draw_kernel (exact ==)
     bool sel_over_max = false;
     int32_t max_slack = 0;      // max over live features of max - selected (draw_lane_kernel: <= 255)
+    // every live feature's need = min - selected stays in [-127, 127] from the start state on (need
+    // only falls, to min - max at worst): draw_lane_kernel's 8-bit need keys (CSA_LANE_KEY8)
+    bool need8 = true;
     // grow-only device scratch + a stream for the repeated small host-API calls
     // (csa_first_panel_not_in: XMIN calls it 5n times)
     void *scratch[32] = {};   // slots 0-7: csa_first_panel_not_in; 8-19: csa_legacy_sample; 20-29: _devices
@@ -1794,6 +1797,15 @@ struct ScopedDevice {
     }
 };
 
+void update_need8(csa_instance *I) {
+    I->need8 = true;
+    for (int f = 0; f < I->F; ++f) {
+        if (I->fmax[f] == 0) continue;  // dead (min = max = 0) or routed elsewhere (max = 0 < min)
+        const int32_t hi = I->fmin[f] - I->sel0[f], lo = I->fmin[f] - I->fmax[f];
+        if (hi > 127 || lo < -127) I->need8 = false;
+    }
+}
+
 int check_k(const csa_instance *I, int32_t k) {
     if (k < 0) return fail(CSA_E_INVALID, "k must be >= 0 (got %d)", k);
     // need*den must stay inside int32 (need = fmin - sel, |need| <= max_abs + k, den <= n)
@@ -1808,6 +1820,7 @@ struct DrawConfig {
     bool lane = false;  // draw_lane_kernel (2 lanes per panel): FPL / WPL hold its FN / WN
     bool wide = false;  // draw_wide_kernel (8 lanes per panel)
     bool solo = false;  // draw_solo_kernel (1 lane per panel): FPL / WPL hold its FN / WN
+    bool k8 = false;    // lane / solo: the 8-bit need keys carrying their index (csa_instance::need8)
     const void *fn = nullptr;
     bool picks() const { return lane || wide || solo; }  // pick-list kernels (picks_pack_kernel builds the panels)
 };
@@ -1837,50 +1850,48 @@ const void *wide_fn(int fpl, int wpl) {
 #ifndef CSA_LANE_SKDIV
 #define CSA_LANE_SKDIV 1
 #endif
-template <int FN, int WN>
+template <int FN, int WN, bool K8>
 const void *lane_fn_wn() {
     constexpr int SK = (WN / 2 + CSA_LANE_SKDIV - 1) / CSA_LANE_SKDIV;
-    return reinterpret_cast<const void *>(&draw_lane_kernel<FN, WN, SK>);
+    return reinterpret_cast<const void *>(&draw_lane_kernel<FN, WN, SK, K8>);
 }
 
-template <int FN>
+template <int FN, bool K8>
 const void *lane_fn_w(int wn) {
     switch (wn) {
-        case 4: return lane_fn_wn<FN, 4>();
-        case 8: return lane_fn_wn<FN, 8>();
-        case 16: return lane_fn_wn<FN, 16>();
-        case 28: return lane_fn_wn<FN, 28>();
-        case 32: return lane_fn_wn<FN, 32>();
+        case 4: return lane_fn_wn<FN, 4, K8>();
+        case 8: return lane_fn_wn<FN, 8, K8>();
+        case 16: return lane_fn_wn<FN, 16, K8>();
+        case 28: return lane_fn_wn<FN, 28, K8>();
+        case 32: return lane_fn_wn<FN, 32, K8>();
         default: return nullptr;
     }
 }
 
-template <int FN>
+template <int FN, bool K8>
 const void *solo_fn_w(int wn) {
     switch (wn) {
-        case 4: return reinterpret_cast<const void *>(&draw_solo_kernel<FN, 4>);
-        case 8: return reinterpret_cast<const void *>(&draw_solo_kernel<FN, 8>);
-        case 16: return reinterpret_cast<const void *>(&draw_solo_kernel<FN, 16>);
-        case 28: return reinterpret_cast<const void *>(&draw_solo_kernel<FN, 28>);
-        case 32: return reinterpret_cast<const void *>(&draw_solo_kernel<FN, 32>);
+        case 4: return reinterpret_cast<const void *>(&draw_solo_kernel<FN, 4, K8>);
+        case 8: return reinterpret_cast<const void *>(&draw_solo_kernel<FN, 8, K8>);
+        case 16: return reinterpret_cast<const void *>(&draw_solo_kernel<FN, 16, K8>);
+        case 28: return reinterpret_cast<const void *>(&draw_solo_kernel<FN, 28, K8>);
+        case 32: return reinterpret_cast<const void *>(&draw_solo_kernel<FN, 32, K8>);
         default: return nullptr;
     }
 }
 
-const void *solo_fn(int fn_, int wn) {
+// k8: the 8-bit need keys with the feature index inside (csa_instance::need8; draw_lane.inc)
+const void *solo_fn(int fn_, int wn, bool k8) {
     switch (fn_) {
-        case 8: return solo_fn_w<8>(wn);
-        case 16: return solo_fn_w<16>(wn);
-#ifdef CSA_SOLO32
-        case 32: return solo_fn_w<32>(wn);
-#endif
+        case 8: return k8 ? solo_fn_w<8, true>(wn) : solo_fn_w<8, false>(wn);
+        case 16: return k8 ? solo_fn_w<16, true>(wn) : solo_fn_w<16, false>(wn);
         default: return nullptr;
     }
 }
 
-const void *lane_fn(int fn_, int wn) {
+const void *lane_fn(int fn_, int wn, bool k8) {
     switch (fn_) {
-        case 32: return lane_fn_w<32>(wn);
+        case 32: return k8 ? lane_fn_w<32, true>(wn) : lane_fn_w<32, false>(wn);
         default: return nullptr;
     }
 }
@@ -1926,21 +1937,19 @@ int pow2_ceil_int(int x) {
 // forces a batch kernel the instance fits (parity tests of every layout).
 int pick_draw_config(const csa_instance *I, bool general, DrawConfig &c) {
     general = general || I->d_addr_next;  // same-address deletions: draw_kernel<64, ..., true> only
-    const bool lane_ok = I->F <= 32 && I->d_pmask && !I->zero_max_min && I->W <= 32 && I->max_abs < 32768 &&
-                         !I->sel_over_max && I->max_slack <= 255;
+    const bool reg_ok = I->F <= 32 && I->d_pmask && !I->zero_max_min && I->W <= 32 && I->max_abs < 32768 &&
+                        !I->sel_over_max && I->max_slack <= 255;
+    const bool lane_ok = reg_ok && I->F > 16;  // built for FN = 32 only
     const bool wide_ok = I->F <= 64 && I->W <= 128 && !I->zero_max_min && I->max_abs < 32768 && !I->sel_over_max;
     const bool g16_ok = I->F <= 64 && I->W <= 256;
     // one lane per panel when a lane holds few features (F <= 16: 142 VGPRs at W = 32, 3 waves/SIMD;
     // example_large_200 281 vs 252 M panels/s, example_small_20 2950 vs 2490); at F = 32 the state needs
     // 165 VGPRs and the two-lane kernel's 4 waves/SIMD win (sf_e 262 vs 247)
-    const bool solo_ok = lane_ok && I->F <= 16;
+    const bool solo_ok = reg_ok && I->F <= 16;
     int choice = general ? 64 : solo_ok ? 1 : lane_ok ? 2 : wide_ok ? 8 : g16_ok ? 16 : 64;
     if (const char *e = getenv("CSA_DRAW_KERNEL")) {
         // the register kernels are built for the shapes they win on only (solo F <= 16, lane F > 16)
         if (!general && !strcmp(e, "solo") && solo_ok) choice = 1;
-#ifdef CSA_SOLO32
-        else if (!general && !strcmp(e, "solo") && lane_ok) choice = 1;
-#endif
         else if (!general && !strcmp(e, "lane") && lane_ok && !solo_ok) choice = 2;
         else if (!general && !strcmp(e, "wide") && wide_ok) choice = 8;
         else if (!general && !strcmp(e, "16") && g16_ok) choice = 16;
@@ -1951,7 +1960,8 @@ int pick_draw_config(const csa_instance *I, bool general, DrawConfig &c) {
         c.solo = true;
         c.FPL = std::max(8, pow2_ceil_int(I->F));
         c.WPL = I->W <= 4 ? 4 : I->W <= 8 ? 8 : I->W <= 16 ? 16 : I->W <= 28 ? 28 : 32;
-        c.fn = solo_fn(c.FPL, c.WPL);
+        c.k8 = I->need8;
+        c.fn = solo_fn(c.FPL, c.WPL, c.k8);
         if (!c.fn) return fail(CSA_E_UNSUPPORTED, "no solo draw kernel for F=%d W=%d", I->F, I->W);
         return CSA_OK;
     }
@@ -1968,7 +1978,8 @@ int pick_draw_config(const csa_instance *I, bool general, DrawConfig &c) {
         c.lane = true;
         c.FPL = std::max(8, pow2_ceil_int(I->F));
         c.WPL = I->W <= 4 ? 4 : I->W <= 8 ? 8 : I->W <= 16 ? 16 : I->W <= 28 ? 28 : 32;
-        c.fn = lane_fn(c.FPL, c.WPL);
+        c.k8 = I->need8;
+        c.fn = lane_fn(c.FPL, c.WPL, c.k8);
         if (!c.fn) return fail(CSA_E_UNSUPPORTED, "no lane draw kernel for F=%d W=%d", I->F, I->W);
         return CSA_OK;
     }
@@ -2329,6 +2340,7 @@ int csa_instance_create(int32_t n, int32_t C, int32_t F, const int32_t *person_f
     I->fcat.assign(feat_cat, feat_cat + F);
     I->pool.assign(F, 0);
     I->sel0.assign(F, 0);
+    update_need8(I);
     I->featmask.assign((size_t)F * I->Ws, 0ull);
     for (int f = 1; f < F; ++f)
         if (feat_cat[f] < feat_cat[f - 1]) {
@@ -2510,6 +2522,7 @@ int csa_instance_set_state(csa_instance *I, const int32_t *sel, const int32_t *r
         if (I->fmax[f] > 0) I->max_slack = std::max(I->max_slack, I->fmax[f] - s);
     }
     I->max_abs = mx;
+    update_need8(I);
     if (present)
         for (int w = 0; w < I->W; ++w)
             if (present[w] & ~all[w]) return fail(CSA_E_INVALID, "present mask has bits beyond n");
@@ -2690,10 +2703,10 @@ int csa_draw_kernel_name(const csa_instance *I, int32_t k, char *buf, uint64_t l
     rc = pick_draw_config(I, false, cfg);
     if (rc) return rc;
     if (cfg.solo)
-        snprintf(buf, (size_t)len, "draw_solo_kernel<%d, %d>", cfg.FPL, cfg.WPL);
+        snprintf(buf, (size_t)len, "draw_solo_kernel<%d, %d, %s>", cfg.FPL, cfg.WPL, cfg.k8 ? "true" : "false");
     else if (cfg.lane)
-        snprintf(buf, (size_t)len, "draw_lane_kernel<%d, %d, %d>", cfg.FPL, cfg.WPL,
-                 (cfg.WPL / 2 + CSA_LANE_SKDIV - 1) / CSA_LANE_SKDIV);
+        snprintf(buf, (size_t)len, "draw_lane_kernel<%d, %d, %d, %s>", cfg.FPL, cfg.WPL,
+                 (cfg.WPL / 2 + CSA_LANE_SKDIV - 1) / CSA_LANE_SKDIV, cfg.k8 ? "true" : "false");
     else if (cfg.wide)
         snprintf(buf, (size_t)len, "draw_wide_kernel<%d, %d, %d>", cfg.G, cfg.FPL, cfg.WPL);
     else

@@ -328,3 +328,37 @@ def test_two_lane_layouts_match_oracle(gpu_available, F_per_cat, n, k, lo, hi, w
     assert np.array_equal(panels, opanels)
     assert stats == {"attempts": int(oatt.sum()), "rejections": int(rejects.sum()),
                      "selection_errors": int(oatt.sum()) - S - int(rejects.sum())}
+
+
+@pytest.mark.parametrize("F_per_cat,n,k,lo,hi,kernel,k8", [
+    ((8, 8, 8, 6), 1700, 110, 0.9, 1.1, "draw_lane_kernel<32, 28", True),
+    ((6, 6, 6), 1900, 600, 0.93, 1.07, "draw_lane_kernel<32, 32", False),   # a min above 127
+    ((3, 3), 1500, 300, 0.95, 1.05, "draw_solo_kernel<8, 28", False),
+    ((3, 3), 1500, 90, 0.9, 1.1, "draw_solo_kernel<8, 28", True),
+])
+def test_key_width_variants_match_oracle(gpu_available, F_per_cat, n, k, lo, hi, kernel, k8):
+    """The register kernels in both key widths: 8-bit need keys carrying the feature index (every
+    need in [-127, 127], the BASELINE shapes) and the 16-bit keys an instance with a min above 127
+    takes -- routing by csa_instance::need8 and panels / attempts / restart counters vs the C oracle."""
+    import ctypes
+    P = pkg()
+    N = pkg("_native")
+    A = pkg("analysis")
+    cats, agents, o = _synthetic_tight(F_per_cat, n, k, seed=n + k + 1, lo=lo, hi=hi)
+    assert (max(o.fmin) <= 127) == k8
+    enc = P.encode(cats, agents)
+    buf = np.zeros(64, np.uint8)
+    N.check(N.lib().csa_draw_kernel_name(enc.handle, k, buf.ctypes.data_as(ctypes.c_char_p), 64))
+    name = bytes(buf).split(b"\0")[0].decode()
+    assert name.startswith(kernel) and name.endswith("true>" if k8 else "false>"), name
+    S, seed, begin = 3000, 11, 4096
+    rejects = np.zeros(S, np.uint32)
+    rc, opanels, oatt, _ = coracle.draw(o, k, seed, begin, S, max_attempts=100000, rejects=rejects)
+    A.draw_stats(enc, reset=True)
+    panels, attempts = _sample(enc, k, S, seed, begin, max_attempts=100000)
+    stats = A.draw_stats(enc)
+    assert rc == 0
+    assert np.array_equal(attempts, oatt)
+    assert np.array_equal(panels, opanels)
+    assert stats == {"attempts": int(oatt.sum()), "rejections": int(rejects.sum()),
+                     "selection_errors": int(oatt.sum()) - S - int(rejects.sum())}
