@@ -32,7 +32,8 @@ CSA_WANT_UNIQUE = 0x8
 CSA_PAIR_FP4 = 0
 CSA_PAIR_I8 = 1
 CSA_PAIR_OVERWRITE = 0x100  # engine flag: store this batch's pair counts instead of adding
-CSA_PAIR_SHARED = 0x200     # engine hint: the launch overlaps concurrent draws (256-register pair waves)
+CSA_PAIR_SHARED = 0x200     # engine hint: the launch overlaps concurrent draws
+CSA_PAIR_ALONE = 0x400      # engine hint: nothing runs beside the launch (the kernel fastest alone)
 
 # every symbol include/csa_legacy.h declares, with its ctypes signature
 _P = ctypes.c_void_p

@@ -1055,8 +1055,9 @@ struct PairMap {
 typedef __attribute__((address_space(3))) void lds_void_t;
 typedef const __attribute__((address_space(1))) void gbl_void_t;
 
-// NB = B fragments per wave.  NB = 4: 128 x 128 wave tiles, 256 x 256 items, 256 accumulators (one
-// wave fills its SIMD's 512 registers).  NB = 2 (CSA_PAIR_SHARED): 128 x 64 wave tiles, 256 x 128 items
+// NB = B fragments per wave.  NB = 4 (every launch): 128 x 128 wave tiles, 256 x 256 items, 256
+// accumulators (one wave fills its SIMD's 512 registers).  NB = 2 (CSA_P2_NB=2, A/B and tests): 128 x 64
+// wave tiles, 256 x 128 items
 // (the column halves of a tile, PairMap::halves = 2), 128 accumulators, at most 256 registers -- a draw
 // workgroup's two 128-VGPR waves per SIMD fit beside it.
 // Every wave streams its own operands -- its 128 A rows and 32 NB B columns of each 64-panel block, two
@@ -2791,7 +2792,10 @@ struct Pair2Plan {
     int grid = 0, lmax = 0;  // persistent workgroups; leftover tiles (pooled over the XCDs)
 };
 
-bool pair2_plan(int32_t n, uint64_t n_blocks, uint32_t engine, bool shared, Pair2Plan &q) {
+// alone (CSA_PAIR_ALONE): no draw runs beside this launch, so the kernel fastest alone is taken --
+// this one wherever it applies (n = 1727: 0.59 vs 0.68 ms per 10^6 panels, 0.50 vs 0.44 of the fp4
+// peak; profiles/r05_pair_alone.txt)
+bool pair2_plan(int32_t n, uint64_t n_blocks, uint32_t engine, bool shared, Pair2Plan &q, bool alone = false) {
     if (engine != CSA_PAIR_FP4 || n_blocks == 0 || n_blocks > kP2MaxBlocks) return false;
     const char *e = getenv("CSA_PAIR_KERNEL");
     const int force = e ? atoi(e) : 0;
@@ -2812,7 +2816,7 @@ bool pair2_plan(int32_t n, uint64_t n_blocks, uint32_t engine, bool shared, Pair
     q.M.nblk = n_blocks;
     q.grid = cus;
     q.lmax = q.M.leftovers();  // pooled leftover tiles (each in pieces(lmax) int32 partial slots)
-    return force == 2 || q.M.ntri >= cus;
+    return force == 2 || alone || q.M.ntri >= cus;
 }
 
 uint64_t pair2_scratch_bytes(const Pair2Plan &q) {
@@ -2821,29 +2825,31 @@ uint64_t pair2_scratch_bytes(const Pair2Plan &q) {
 }  // namespace
 
 uint64_t csa_pair_scratch_bytes(int32_t n, uint64_t n_blocks, uint32_t engine) {
-    engine &= ~(CSA_PAIR_OVERWRITE | CSA_PAIR_SHARED);
+    engine &= ~(CSA_PAIR_OVERWRITE | CSA_PAIR_SHARED | CSA_PAIR_ALONE);
     if (n <= 0 || n_blocks == 0) return 0;
-    // enough for either form of the per-CU kernel, so one buffer serves calls with and without
-    // CSA_PAIR_SHARED
-    Pair2Plan q, q2;
-    if (pair2_plan(n, n_blocks, engine, false, q) && pair2_plan(n, n_blocks, engine, true, q2))
-        return std::max<uint64_t>(std::max(pair2_scratch_bytes(q), pair2_scratch_bytes(q2)), 4);
+    // enough for every form a call may take (per-CU kernel with or without CSA_PAIR_SHARED /
+    // CSA_PAIR_ALONE, or the split kernel), so one buffer serves all of them
+    uint64_t need = 0;
+    Pair2Plan q;
+    if (pair2_plan(n, n_blocks, engine, false, q, true)) need = std::max<uint64_t>(pair2_scratch_bytes(q), 4);
+    if (pair2_plan(n, n_blocks, engine, false, q)) return need;
     PairPlan p;
-    if (pair_plan(n, n_blocks, engine, p)) return 0;
-    return (uint64_t)p.ntri * p.nsplit * kPairBlock * kPairBlock * sizeof(int32_t);
+    if (pair_plan(n, n_blocks, engine, p)) return need;
+    return std::max<uint64_t>(need, (uint64_t)p.ntri * p.nsplit * kPairBlock * kPairBlock * sizeof(int32_t));
 }
 
 int csa_pair_counts_ex_async(const uint64_t *d_xt, uint64_t n_blocks, int32_t n, int64_t *d_pairs,
                              uint32_t engine, void *d_scratch, uint64_t scratch_bytes, void *stream) {
     if (n <= 0 || !d_xt || !d_pairs) return fail(CSA_E_INVALID, "pairs: bad arguments");
     const bool overwrite = (engine & CSA_PAIR_OVERWRITE) != 0u, shared = (engine & CSA_PAIR_SHARED) != 0u;
-    engine &= ~(CSA_PAIR_OVERWRITE | CSA_PAIR_SHARED);
+    const bool alone = (engine & CSA_PAIR_ALONE) != 0u && !shared;
+    engine &= ~(CSA_PAIR_OVERWRITE | CSA_PAIR_SHARED | CSA_PAIR_ALONE);
     const hipStream_t st = (hipStream_t)stream;
     if (overwrite && (n_blocks == 0 || !d_scratch))  // no reduce pass to store every element
         HIPCHK(hipMemsetAsync(d_pairs, 0, (size_t)n * n * sizeof(int64_t), st));
     if (n_blocks == 0) return CSA_OK;
     Pair2Plan q;
-    if (d_scratch && pair2_plan(n, n_blocks, engine, shared, q)) {
+    if (d_scratch && pair2_plan(n, n_blocks, engine, shared, q, alone)) {
         if (scratch_bytes < pair2_scratch_bytes(q))
             return fail(CSA_E_INVALID, "pairs: scratch of %llu B < csa_pair_scratch_bytes = %llu B",
                         (unsigned long long)scratch_bytes, (unsigned long long)pair2_scratch_bytes(q));

@@ -144,17 +144,19 @@ class DevicePipeline:
                                                   N.ptr(self.xt) if self.want_pairs else None,
                                                   N.ptr(self.counts), _stream_ptr(self.stream)))
 
-    def pair_counts(self, S, overwrite=False, shared=False):
+    def pair_counts(self, S, overwrite=False, shared=False, alone=False):
         """Pair counts of the batch into self.pairs: added (default) or, with ``overwrite``, stored
         (upper triangle incl. the diagonal; CSA_PAIR_OVERWRITE, no zero-fill needed).  ``shared``:
-        the launch overlaps draws on another stream (CSA_PAIR_SHARED, a scheduling hint)."""
+        the launch overlaps draws on another stream (CSA_PAIR_SHARED, a scheduling hint); ``alone``:
+        no draw runs beside it (CSA_PAIR_ALONE: the kernel fastest alone)."""
         nblk = (int(S) + 63) // 64
         L = N.lib()
         need = int(L.csa_pair_scratch_bytes(self.enc.n, nblk, self.pair_engine))
         assert need <= self.pair_scratch.numel() * 4
         N.check(L.csa_pair_counts_ex_async(N.ptr(self.xt), nblk, self.enc.n, N.ptr(self.pairs),
                                            self.pair_engine | (N.CSA_PAIR_OVERWRITE if overwrite else 0)
-                                           | (N.CSA_PAIR_SHARED if shared else 0),
+                                           | (N.CSA_PAIR_SHARED if shared else 0)
+                                           | (N.CSA_PAIR_ALONE if alone else 0),
                                            N.ptr(self.pair_scratch), self.pair_scratch.numel() * 4,
                                            _stream_ptr(self.stream)))
 
@@ -211,7 +213,9 @@ class DevicePipeline:
                 self.panels = panels[off * W:(off + ln) * W]
                 self.transpose_count(ln)
                 if self.want_pairs:
-                    self.pair_counts(ln, overwrite=overwrite_pairs and j == 0, shared=j + 1 < len(chunks))
+                    # the last chunk's pairs run after every draw of the call: the kernel fastest alone
+                    self.pair_counts(ln, overwrite=overwrite_pairs and j == 0, shared=j + 1 < len(chunks),
+                                     alone=j + 1 == len(chunks))
         finally:
             self.panels, self.hashes = own_p, own_h
 

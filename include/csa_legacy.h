@@ -270,11 +270,14 @@ int csa_transpose_count_async(const uint64_t *d_panels, uint64_t n_panels, int32
  * scheduling hint, never a change of result: the launch will share the CUs with
  * concurrent draw kernels (a pipelined caller).  The library currently takes the
  * same 512-register per-CU form either way (measured faster beside the draws than
- * the 256-register form, which CSA_P2_NB=2 still selects). */
+ * the 256-register form, which CSA_P2_NB=2 still selects).  engine | CSA_PAIR_ALONE
+ * is the opposite hint: nothing runs beside the launch (a serial caller's last
+ * batch), so the kernel fastest alone is taken (the per-CU kernel at any n). */
 #define CSA_PAIR_FP4 0u
 #define CSA_PAIR_I8 1u
 #define CSA_PAIR_OVERWRITE 0x100u
 #define CSA_PAIR_SHARED 0x200u
+#define CSA_PAIR_ALONE 0x400u
 uint64_t csa_pair_scratch_bytes(int32_t n, uint64_t n_blocks, uint32_t engine);
 int csa_pair_counts_ex_async(const uint64_t *d_xt, uint64_t n_blocks, int32_t n, int64_t *d_pairs,
                              uint32_t engine, void *d_scratch, uint64_t scratch_bytes, void *stream);

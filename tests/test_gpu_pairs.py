@@ -173,12 +173,15 @@ def test_pairs_n8192_vs_torch_fp32(gpu_available, pair_kernel, engine, n):
 
 @pytest.mark.parametrize("n,nblk", [(20, 1), (20, 31), (257, 3), (1727, 40), (4100, 7), (8192, 33)])
 @pytest.mark.parametrize("overwrite", [True, False])
-@pytest.mark.parametrize("shared", [False, True])
-def test_pair_tile_kernel_small_and_ragged(gpu_available, monkeypatch, n, nblk, overwrite, shared):
-    """pair_fp4_tile_kernel edge cases, both forms (CSA_PAIR_SHARED: 256 x 128 column-half items): fewer
-    panel blocks than k-pieces (empty pieces), one tile only (n = 20: one XCD has work), XCD chunks with
-    and without leftover items, n not a multiple of 256, a column half wholly past n (n = 4100)."""
+@pytest.mark.parametrize("nb", [4, 2])
+def test_pair_tile_kernel_small_and_ragged(gpu_available, monkeypatch, n, nblk, overwrite, nb):
+    """pair_fp4_tile_kernel edge cases, both forms (CSA_P2_NB=4: 256 x 256 tiles; CSA_P2_NB=2: 256 x 128
+    column-half items, PairMap::halves = 2): fewer panel blocks than k-pieces (empty pieces), one tile
+    only (n = 20: one XCD has work), XCD chunks with and without leftover items, n not a multiple of
+    256, a column half wholly past n (n = 4100) and the leftover reduce of half items."""
     monkeypatch.setenv("CSA_PAIR_KERNEL", "2")
+    monkeypatch.setenv("CSA_P2_NB", str(nb))
+    shared = nb == 2              # the scheduling hint changes nothing; exercised beside the NB = 2 form
     N = pkg("_native")
     npad = int(N.lib().csa_xt_pad(n))
     rng = np.random.default_rng(n * 31 + nblk)
