@@ -8,7 +8,8 @@ import numpy as np
 from .legacy_oracle import OracleInstance
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-_LIB_PATH = os.path.join(_HERE, "_build", "liblegacy_oracle.so")
+# CSA_ORACLE_LIB: another build of the same source (tools/asan_host.sh: the sanitizer build)
+_LIB_PATH = os.environ.get("CSA_ORACLE_LIB") or os.path.join(_HERE, "_build", "liblegacy_oracle.so")
 _lib = None
 
 P = ctypes.c_void_p
