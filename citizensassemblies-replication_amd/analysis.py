@@ -2,13 +2,16 @@
 
 Kept names and semantics (reference file:line):
   * ``Instance``, ``read_instance``    analysis.py:54-58, 108-138 (from .instance)
-  * ``PairHistogram``                  analysis.py:68-98 -- same methods, backed by a
-                                       dense count matrix instead of an n(n-1)/2 dict
+  * ``PairHistogram``                  analysis.py:68-98 -- same methods, backed by one
+                                       packed array of the n(n-1)/2 pair values (row-major
+                                       i < j) instead of a dict, filled on the device
   * ``legacy_find``                    analysis.py:141-159 -- restarts run on the device
   * ``legacy_probabilities``           analysis.py:162-191 -- the batch entry point:
-                                       draw S panels (one per wavefront), per-person
-                                       counts, X^T X pair counts on int8 MFMA,
-                                       distinct-panel count; returns
+                                       draw S panels (each panel's state in the registers
+                                       of 1, 2 or 8 lanes of a wavefront, by instance
+                                       shape), per-person counts, X^T X pair counts on fp4
+                                       MFMA (exact 0/1 products, f32 accumulation; int8
+                                       selectable), exact distinct-panel count; returns
                                        ``(alloc, found_panels, pair_histogram)``.
 LEXIMIN / XMIN and the plotting / statistics code stay in the reference (CPU).
 """
