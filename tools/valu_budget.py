@@ -38,26 +38,40 @@ QUAD = 4.0   # SQ_ACTIVE_INST_VALU counts one quad-cycle per VALU instruction of
 
 
 def regions(text, needle):
+    """Static VALU per region in layout order.  The compiler sinks the pick's every-step work (pick-list
+    accumulation, key / slack decrements, pool drop) below the conditional pick-list store, so inside the
+    "store" region only the instructions under the store's exec mask (s_and_saveexec ... s_or_b64 exec)
+    count as "store"; the rest of that region runs with every pick ("update")."""
     body = kernel_body(text, needle)
     cur = "prologue"
     per = collections.defaultdict(collections.Counter)
     ops = collections.defaultdict(collections.Counter)
     seen_loop = False
+    in_store = None          # the saved-exec SGPRs of the store branch while inside it
     for raw in body.splitlines():
         m = re.search(r";@region (\w+)", raw)
         if m:
             cur = m.group(1)
             seen_loop = True
+            in_store = None
             continue
         line = raw.split(";")[0].strip()
         if not line or line.startswith((".", "_")) or line.endswith(":"):
             continue
+        reg = cur if seen_loop else "prologue"
+        if cur == "store":
+            ms = re.match(r"s_and_saveexec_b64 (s\[\d+:\d+\]), vcc", line)
+            if ms and in_store is None:
+                in_store = ms.group(1)
+            elif in_store and line.startswith("s_or_b64 exec, exec, " + in_store):
+                in_store = ""            # past the store's join: the rest runs with every pick
+            reg = "store" if in_store else "update"
         name, cls = classify(line)
         if name is None:
             continue
         # code laid out after the last marker that closes the loop (the fused pack / exit) is the tail
-        per[cur if seen_loop else "prologue"][cls] += 1
-        ops[cur if seen_loop else "prologue"][name] += 1
+        per[reg][cls] += 1
+        ops[reg][name] += 1
     return per, ops
 
 
@@ -66,7 +80,7 @@ def main():
     ap.add_argument("asm")
     ap.add_argument("stamps", help="tools/lane_stamps.py JSON (region_runs_per_wave, ms, panels, waves)")
     ap.add_argument("--pmc", help="profiles/pmc_<config>.json (draw_issue: VALU per panel, clock)")
-    ap.add_argument("--kernel", default="draw_lane_kernelILi32ELi28ELi14E")
+    ap.add_argument("--kernel", default="draw_lane_kernelILi32ELi28ELi14ELb1E")
     ap.add_argument("--panels-per-wave", type=int, default=32)
     ap.add_argument("--out")
     args = ap.parse_args()
