@@ -434,17 +434,25 @@ def legacy_sample_device(enc, k, S, random_seed, keep_panels=True, chunk=1 << 20
         panels = torch.empty(max(S * W, 1), dtype=torch.int64, device=dev)
         hashes = torch.empty(max(2 * S, 2), dtype=torch.int64, device=dev)
         pairs = torch.empty(enc.n * enc.n, dtype=torch.int64, device=dev)
-        pipe.reset(pairs=False)
+        # status before the draws; the counters after the draws are enqueued (the draw stream does not
+        # wait for them, the counting on this stream does)
+        pipe.reset(pairs=False, counts=host_panels is not None)
         if host_panels is None:
             reset_draw_stats(enc, pipe.stream)
         own_p, own_h, own_pairs = pipe.panels, pipe.hashes, pipe.pairs
         pipe.pairs = pairs
+        # the distinct-count table (zero-filled on allocation, on this stream) before the draws: the
+        # draw stream waits on this stream, and the distinct count's side stream on the draw stream
+        table = getattr(enc, "_table", None)
+        if table is None:
+            table = enc._table = HashTable(S, dev)
+        table.ensure(S)
         try:
             if host_panels is None:
                 # chunk draws on the pipeline's draw stream, counting and pairs on its stream, overlapped
                 # (DevicePipeline.draw_count_chunks); two draw streams were measured slower
                 # (profiles/r04f_draw_streams/)
-                pipe.draw_count_chunks(random_seed, 0, S, panels, hashes, C, overwrite_pairs=True)
+                pipe.draw_count_chunks(random_seed, 0, S, panels, hashes, C, overwrite_pairs=True, reset_counts=True)
             else:
                 for off in range(0, S, C):
                     ln = min(C, S - off)
@@ -456,14 +464,23 @@ def legacy_sample_device(enc, k, S, random_seed, keep_panels=True, chunk=1 << 20
                     pipe.pair_counts(ln, overwrite=off == 0)
             if S == 0:
                 pairs.zero_()
-            table = getattr(enc, "_table", None)
-            if table is None:
-                table = enc._table = HashTable(S, dev)
-            table.ensure(S)
-            table.count.zero_()
-            N.check(N.lib().csa_unique_async(N.ptr(hashes), N.ptr(panels), S, W, N.ptr(table.table), table.slots,
-                                             N.ptr(table.count), N.ptr(pipe.status),
-                                             ctypes.c_void_p(pipe.stream.cuda_stream)))
+            # the distinct count needs only the draws (hashes, panels): with device draws it runs on a
+            # side stream beside the counting and pairs of the last chunk, and the pipeline stream
+            # waits for it before the one host read.  Everything it touches is ordered on that stream:
+            # the counter reset, the table, and the hand-back (pipeline stream waits on the side stream)
+            ust = pipe.stream
+            if host_panels is None:
+                ust = getattr(pipe, "unique_stream", None)
+                if ust is None:
+                    ust = pipe.unique_stream = torch.cuda.Stream(dev)
+                ust.wait_stream(pipe.draw_stream)  # (the draw stream itself waited on the pipeline stream)
+            with torch.cuda.stream(ust):
+                table.count.zero_()
+                N.check(N.lib().csa_unique_async(N.ptr(hashes), N.ptr(panels), S, W, N.ptr(table.table), table.slots,
+                                                 N.ptr(table.count), N.ptr(pipe.status),
+                                                 ctypes.c_void_p(ust.cuda_stream)))
+            if ust is not pipe.stream:
+                pipe.stream.wait_stream(ust)
             # counts, distinct count, draw statistics and status in ONE copy: the call's one host wait
             parts = [pipe.counts, table.count]
             if host_panels is None:
@@ -544,7 +561,8 @@ def legacy_probabilities(instance: Instance, iterations: int, random_seed: int,
 def finish(instance, enc, raw, S):
     global LAST_RUN_STATS
     LAST_RUN_STATS = raw.stats
-    alloc = {aid: int(raw.counts[p]) / S for p, aid in enumerate(enc.agent_ids)}
+    # int / int true division, as the reference's count / S (one tolist, no per-element numpy indexing)
+    alloc = {aid: c / S for aid, c in zip(enc.agent_ids, np.asarray(raw.counts).tolist())}
     hist = PairHistogram(len(instance.agents), counts=raw.pairs)
     hist.turn_into_probabilities_by_dividing_all_elements_by_given_number(S)
     hist._counts, hist._S = raw.pairs, S      # integer counts for stats.sorted_pair_probabilities

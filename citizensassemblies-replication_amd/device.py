@@ -92,14 +92,17 @@ class DevicePipeline:
             self.table = torch.empty(slots, dtype=u64, device=dev) if want_unique else None
             self.unique = torch.zeros(1, dtype=torch.int64, device=dev)
 
-    def reset(self, status=True, pairs=True):
+    def reset(self, status=True, pairs=True, counts=True):
         """Zero the accumulators.  ``pairs=False`` skips the n*n pair matrix for a caller whose next
-        ``pair_counts(..., overwrite=True)`` stores the batch's counts instead of adding them."""
+        ``pair_counts(..., overwrite=True)`` stores the batch's counts instead of adding them;
+        ``counts=False`` leaves the counts and the distinct count (draw_count_chunks(reset_counts=True)
+        zeroes the counts after the draws are enqueued)."""
         with torch.cuda.stream(self.stream):
             if status:
                 self.status.zero_()
-            self.counts.zero_()
-            self.unique.zero_()
+            if counts:
+                self.counts.zero_()
+                self.unique.zero_()
             if pairs and self.pairs is not None:
                 self.pairs.zero_()
 
@@ -176,14 +179,17 @@ class DevicePipeline:
             rp = self._round = max(1, int(out[0]))
         return rp
 
-    def draw_count_chunks(self, seed, panel_begin, S, panels, hashes, chunk, overwrite_pairs=False):
+    def draw_count_chunks(self, seed, panel_begin, S, panels, hashes, chunk, overwrite_pairs=False,
+                          reset_counts=False):
         """Draw S panels (global indices panel_begin ..) into ``panels`` / ``hashes`` (tensors of the
         whole batch) and accumulate their counts and pairs, in chunks of at most ``chunk`` panels
         (at most max_panels): every chunk's draw is enqueued at once on the pipeline's draw stream, each into
         its own slice, and the pipeline stream counts and pairs chunk c after chunk c's draw event --
         beside the draw of chunk c + 1 (bench.py's pipeline).  The first chunk stores its pair counts
         with ``overwrite_pairs``; later chunks add theirs.  Ordered after everything already on the
-        pipeline stream; on return the pipeline stream is ordered after every draw."""
+        pipeline stream; on return the pipeline stream is ordered after every draw.  ``reset_counts``:
+        the per-person counts are zeroed on the pipeline stream after the draws are enqueued (before
+        the first chunk's counting), so the draws do not wait for it."""
         import os
         import torch
         S, C, W = int(S), max(1, min(int(chunk), self.max_panels)), self.enc.W
@@ -208,6 +214,9 @@ class DevicePipeline:
                 ev = torch.cuda.Event()
                 ev.record(st)
                 drawn.append(ev)
+            if reset_counts:
+                with torch.cuda.stream(self.stream):
+                    self.counts.zero_()
             for j, (off, ln) in enumerate(chunks):
                 self.stream.wait_event(drawn[j])
                 self.panels = panels[off * W:(off + ln) * W]

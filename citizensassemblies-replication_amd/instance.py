@@ -119,11 +119,16 @@ class EncodedInstance:
             pass
 
     def check_quotas(self, k):
-        """analysis.py:174-176 (AssertionError, as the reference)."""
+        """analysis.py:174-176 (AssertionError, as the reference).  A passing k is remembered (the
+        encoding's quotas never change)."""
+        ok = self.__dict__.setdefault("_quota_ok", set())
+        if k in ok:
+            return
         for c in range(self.C):
             m = self.fcat == c
             assert int(self.fmin[m].sum()) <= k
             assert int(self.fmax[m].sum()) >= k
+        ok.add(k)
 
     # -- helpers ---------------------------------------------------------------------------
     def present_mask(self, keys=None):
