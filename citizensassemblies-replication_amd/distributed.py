@@ -533,6 +533,9 @@ def legacy_probabilities_distributed(instance, iterations, random_seed, keep_pan
         calls ``found_panels.gather()`` (the collective, checked to be the same run on all ranks).
         Iterating, testing membership, comparing or pickling an un-gathered set raises at once on
         any rank -- it never enters a collective by itself.
+    One rank (no exchange): no collective at all; the distinct count runs on a side stream beside the
+    last counting, and found_panels keeps the panels on the device and decodes them when iterated, as
+    the one-GPU call does (``gather`` changes nothing, ``found_panels.gather()`` is a no-op).
     The draw statistics (analysis.LAST_RUN_STATS) are summed over ranks.  ``timings`` (a dict) gets
     the host-side stage times in ms."""
     import time
@@ -575,6 +578,11 @@ def legacy_probabilities_distributed(instance, iterations, random_seed, keep_pan
         acc = torch.zeros(n + 4, dtype=torch.int64, device=dev)
         pipe.reset(pairs=False)
         A.reset_draw_stats(enc, st)
+        if ex is None:  # one rank: its distinct-count table before the draws (see below)
+            table = getattr(enc, "_table", None)
+            if table is None:
+                table = enc._table = HashTable(local, dev)
+            table.ensure(local)
         own_counts, own_pairs = pipe.counts, pipe.pairs
         pipe.counts, pipe.pairs = acc[:n], pairs
         try:
@@ -586,23 +594,30 @@ def legacy_probabilities_distributed(instance, iterations, random_seed, keep_pan
             pipe.counts, pipe.pairs = own_counts, own_pairs
         # this shard's draw statistics, before the exchange's re-draws (device, no host wait)
         N.check(L.csa_instance_draw_stats_async(enc.handle, N.ptr(acc[n:n + 3]), sp))
-        _all_reduce_pairs(pairs, S, st)
         if ex is not None:
+            _all_reduce_pairs(pairs, S, st)
             u = ex.run(hashes, panels, local, status=pipe.status, stream=st, panel_begin=begin,
                        redraw=(enc.handle, k, random_seed, 0))
-        else:           # one rank owns every panel: the exact local count, no exchange
-            table = getattr(enc, "_table", None)
-            if table is None:
-                table = enc._table = HashTable(local, dev)
-            table.ensure(local)
-            table.count.zero_()
-            N.check(L.csa_unique_async(N.ptr(hashes), N.ptr(panels), local, W, N.ptr(table.table), table.slots,
-                                       N.ptr(table.count), N.ptr(pipe.status), sp))
+        else:
+            # one rank owns every panel: nothing to reduce, and the exact local distinct count runs on
+            # a side stream after the draws, beside the last chunk's counting and pairs (as
+            # analysis.legacy_sample_device; the table was allocated before the draws were enqueued)
+            ust = getattr(pipe, "unique_stream", None)
+            if ust is None:
+                ust = pipe.unique_stream = torch.cuda.Stream(dev)
+            ust.wait_stream(pipe.draw_stream if local else st)
+            with torch.cuda.stream(ust):
+                table.count.zero_()
+                N.check(L.csa_unique_async(N.ptr(hashes), N.ptr(panels), local, W, N.ptr(table.table),
+                                           table.slots, N.ptr(table.count), N.ptr(pipe.status),
+                                           ctypes.c_void_p(ust.cuda_stream)))
+            st.wait_stream(ust)
             u = table.count
         acc[n + 3:].copy_(u)
-        _all_reduce(acc)
         code = pipe.status[:1].to(torch.int64)
-        _all_reduce(code, op=dist.ReduceOp.MAX)
+        if ex is not None:
+            _all_reduce(acc)
+            _all_reduce(code, op=dist.ReduceOp.MAX)
         tail = torch.cat([code, pipe.status.to(torch.int64)])
         host = torch.cat([acc, tail]).cpu()          # the call's one host wait
     t2 = time.perf_counter()
@@ -611,9 +626,12 @@ def legacy_probabilities_distributed(instance, iterations, random_seed, keep_pan
         _decode_status((h[n + 5:n + 9] & 0xFFFFFFFF).astype(np.uint32), int(h[n + 4]))
     counts = h[:n].copy()
     stats = dict(zip(A.STAT_KEYS, (int(x) for x in h[n:n + 3])))
-    raw = A.LegacyRaw(counts, pairs.view(n, n), int(h[n + 3]), None, None, stats)
+    # one rank (no exchange): its panels are the whole run's, so found_panels keeps them on the device and
+    # decodes them when iterated, as the one-GPU call does -- there is nothing to gather
+    solo = ex is None and keep_panels
+    raw = A.LegacyRaw(counts, pairs.view(n, n), int(h[n + 3]), panels[: local * W] if solo else None, None, stats)
     out = A.finish(instance, enc, raw, S)
-    if keep_panels:
+    if keep_panels and not solo:
         sg = ShardGather(hashes[: 2 * local], panels[: local * W], local, W, st, run_id=run_id)
         out[1]._root = r == 0
         out[1]._where = "found_panels of a sharded run iterate on rank 0 only (len() is global)"
