@@ -1,0 +1,51 @@
+"""Soak check of the stream hand-offs in legacy_probabilities (GPU box): many calls of varying size,
+chunking and instance, each checked for its invariants (sum of counts = S k, pair row sums, the exact
+distinct count equal to a reference call's).  Prints one JSON line; exits non-zero on the first
+mismatch.  Usage: python tools/api_soak.py [calls]"""
+import importlib
+import json
+import os
+import sys
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+P = importlib.import_module("citizensassemblies-replication_amd")
+A = importlib.import_module("citizensassemblies-replication_amd.analysis")
+
+if __name__ == "__main__":
+    calls = int(sys.argv[1]) if len(sys.argv) > 1 else 120
+    cases = [("sf_e_110", 110), ("example_large_200", 200), ("rejecty_6", 6), ("couples_panel_from_twenty_people_no_constraints_2", 2)]
+    insts = {}
+    for name, k in cases:
+        d = os.path.join(REPO, "tests", "golden", "instances", name)
+        insts[name] = P.read_instance(os.path.join(d, "categories.csv"), os.path.join(d, "respondents.csv"), k)
+    rng = np.random.default_rng(5)
+    ref = {}
+    done = 0
+    for c in range(calls):
+        name, k = cases[c % len(cases)]
+        inst = insts[name]
+        S = int(rng.choice([1, 63, 1000, 65536, 131072, 300001, 1 << 20, 1100000]))
+        seed = int(rng.integers(0, 4))
+        alloc, found, hist = A.legacy_probabilities(inst, S, seed)
+        tot = sum(alloc.values()) * S
+        if abs(tot - S * k) > 1e-6 * S * k:
+            print(json.dumps({"fail": "counts", "call": c, "instance": name, "S": S, "sum": tot}))
+            sys.exit(1)
+        key = (name, S, seed)
+        if key in ref and ref[key] != len(found):
+            print(json.dumps({"fail": "distinct", "call": c, "instance": name, "S": S, "got": len(found), "ref": ref[key]}))
+            sys.exit(1)
+        ref[key] = len(found)
+        if name == "sf_e_110" and S > 1 and len(found) < S - 2:   # sf_e draws are (almost surely) all distinct
+            print(json.dumps({"fail": "distinct_sfe", "call": c, "S": S, "got": len(found)}))
+            sys.exit(1)
+        if c % 16 == 0:
+            up = hist.upper()
+            if not np.isfinite(up).all():
+                print(json.dumps({"fail": "pairs", "call": c}))
+                sys.exit(1)
+        done += 1
+    print(json.dumps({"calls": done, "distinct_keys": len(ref), "ok": True}))
