@@ -75,6 +75,8 @@ SIGNATURES = {
     "csa_pairs_pack_async": (ctypes.c_int, [_P, _I32, _P, _P]),
     "csa_pairs_unpack_async": (ctypes.c_int, [_P, _I32, _P, _P]),
     "csa_pairs_upper_async": (ctypes.c_int, [_P, _I32, ctypes.c_double, _P, _P]),
+    "csa_pairs_diag_async": (ctypes.c_int, [_P, _I32, _P, _P]),
+    "csa_draw_xt_async": (ctypes.c_int, [_P, _I32, _U64, _U64, _U64, _U32, _P, _P, _P, _P, _P, _P, _P]),
     "csa_status_decode": (ctypes.c_int, [_P]),
     "csa_legacy_draw_mt": (ctypes.c_int, [_I32, _I32, _I32, _P, _P, _P, _P, _P, _P, _P, _I32, _P, _U64, _U32,
                                           _I32, _P, _P, _P, _P, _P, _P, _P]),

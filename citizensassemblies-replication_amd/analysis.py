@@ -16,6 +16,7 @@ Kept names and semantics (reference file:line):
 LEXIMIN / XMIN and the plotting / statistics code stay in the reference (CPU).
 """
 import ctypes
+import os
 from typing import Dict, List, Tuple
 
 import numpy as np
@@ -448,7 +449,22 @@ def legacy_sample_device(enc, k, S, random_seed, keep_panels=True, chunk=1 << 20
             table = enc._table = HashTable(S, dev)
         table.ensure(S)
         try:
-            if host_panels is None:
+            drawn = None  # what the distinct count's side stream waits for: the draws
+            if host_panels is None and 0 < S <= C and os.environ.get("CSA_DRAW_XT", "1") != "0":
+                # one chunk: draw on the pipeline stream; draw_lane_kernel's fused pack also writes the XT
+                # blocks (csa_draw_xt_async), so the counting is the pair kernel alone and the counts
+                # are the pair diagonal -- the transpose pass leaves the call's serial tail
+                pipe.panels, pipe.hashes = panels[:S * W], hashes[:2 * S]
+                xt_done = pipe.draw_xt(random_seed, 0, S)
+                drawn = torch.cuda.Event()
+                drawn.record(pipe.stream)
+                if not xt_done:
+                    pipe.counts.zero_()
+                    pipe.transpose_count(S)
+                pipe.pair_counts(S, overwrite=True, alone=True)
+                if xt_done:
+                    pipe.counts_from_pairs()
+            elif host_panels is None:
                 # chunk draws on the pipeline's draw stream, counting and pairs on its stream, overlapped
                 # (DevicePipeline.draw_count_chunks); two draw streams were measured slower
                 # (profiles/r04f_draw_streams/)
@@ -473,7 +489,10 @@ def legacy_sample_device(enc, k, S, random_seed, keep_panels=True, chunk=1 << 20
                 ust = getattr(pipe, "unique_stream", None)
                 if ust is None:
                     ust = pipe.unique_stream = torch.cuda.Stream(dev)
-                ust.wait_stream(pipe.draw_stream)  # (the draw stream itself waited on the pipeline stream)
+                if drawn is not None:
+                    ust.wait_event(drawn)
+                else:
+                    ust.wait_stream(pipe.draw_stream)  # (the draw stream itself waited on the pipeline stream)
             with torch.cuda.stream(ust):
                 table.count.zero_()
                 N.check(N.lib().csa_unique_async(N.ptr(hashes), N.ptr(panels), S, W, N.ptr(table.table), table.slots,

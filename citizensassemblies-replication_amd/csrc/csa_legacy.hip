@@ -140,6 +140,11 @@ struct DrawArgs {
     const unsigned long long *n_panels_dev;
     int32_t *sel_out, *rem_out;
     uint64_t *present_out;
+    // csa_draw_xt_async (draw_lane_kernel's fused pack only): the launch's panels also as XT (the
+    // pair kernels' operand, csa_transpose_count_async's layout: two 32-bit planes per 64-panel block,
+    // npad persons each) or null
+    uint32_t *xt;
+    int32_t npad;
 };
 
 // ---- sub-wave group primitives ------------------------------------------------------------
@@ -575,32 +580,6 @@ __global__ __launch_bounds__(draw_threads(FPL, WPL), draw_occupancy(FPL, WPL)) v
     }
 }
 
-#include "draw_lane.inc"
-#include "draw_wide.inc"
-#include "draw_solo.inc"
-
-// 128-bit panel hashes (the draw_kernel's in-kernel hash, for the batch kernel's panels): a
-// quad of lanes per panel, words glane, glane+4, ... (coalesced within the quad), quad sum.
-__global__ __launch_bounds__(256) void panel_hash_kernel(const uint64_t *__restrict__ panels, uint64_t S, int W,
-                                                         uint64_t *__restrict__ hashes) {
-    const uint64_t i = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 2;
-    const int q = threadIdx.x & 3;
-    uint64_t h1 = 0, h2 = 0;
-    if (i < S) {
-        for (int w = q; w < W; w += 4) {
-            const uint64_t pk = panels[i * W + w];
-            h1 += fmix_a(pk ^ ((uint64_t)w * 0x9E3779B97F4A7C15ull));
-            h2 += fmix_b(pk + ((uint64_t)w + 1) * 0xD6E8FEB86659FD93ull);
-        }
-    }
-    h1 = group_sum64<0, 2>(h1);
-    h2 = group_sum64<0, 2>(h2);
-    if (i < S && q == 0) {
-        hashes[2 * i] = h1;
-        hashes[2 * i + 1] = h2;
-    }
-}
-
 // ------------------------------------------------------------------------------------------
 // Bit transpose + per-person counts
 // ------------------------------------------------------------------------------------------
@@ -672,6 +651,32 @@ __device__ __forceinline__ void wave_transpose64(uint32_t &lo, uint32_t &hi, con
     hi = xt_merge(hi, xt_dpp<0x4E>(hi), c.k2, c.r2);
     lo = xt_merge(lo, xt_dpp<0xB1>(lo), c.k1, c.r1);  // s = 1: quad_perm [1,0,3,2]
     hi = xt_merge(hi, xt_dpp<0xB1>(hi), c.k1, c.r1);
+}
+
+#include "draw_lane.inc"
+#include "draw_wide.inc"
+#include "draw_solo.inc"
+
+// 128-bit panel hashes (the draw_kernel's in-kernel hash, for the batch kernel's panels): a
+// quad of lanes per panel, words glane, glane+4, ... (coalesced within the quad), quad sum.
+__global__ __launch_bounds__(256) void panel_hash_kernel(const uint64_t *__restrict__ panels, uint64_t S, int W,
+                                                         uint64_t *__restrict__ hashes) {
+    const uint64_t i = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 2;
+    const int q = threadIdx.x & 3;
+    uint64_t h1 = 0, h2 = 0;
+    if (i < S) {
+        for (int w = q; w < W; w += 4) {
+            const uint64_t pk = panels[i * W + w];
+            h1 += fmix_a(pk ^ ((uint64_t)w * 0x9E3779B97F4A7C15ull));
+            h2 += fmix_b(pk + ((uint64_t)w + 1) * 0xD6E8FEB86659FD93ull);
+        }
+    }
+    h1 = group_sum64<0, 2>(h1);
+    h2 = group_sum64<0, 2>(h2);
+    if (i < S && q == 0) {
+        hashes[2 * i] = h1;
+        hashes[2 * i + 1] = h2;
+    }
 }
 
 // blockIdx.y = column range: words [CW y, CW y + CW) of every panel, i.e. agents [64 CW y, ...).
@@ -1680,6 +1685,15 @@ __global__ __launch_bounds__(256) void pairs_unpack_kernel(const int32_t *__rest
     for (int j = i + (int)threadIdx.x; j < n; j += blockDim.x) pairs[(uint64_t)i * n + j] = packed[off + (j - i)];
 }
 
+// per-person counts = the pair matrix's diagonal (sum over panels of x_i^2 = x_i): csa_pairs_diag_async,
+// the counts of a draw whose XT came from the draw kernel (csa_draw_xt_async) instead of
+// csa_transpose_count_async
+__global__ __launch_bounds__(256) void pairs_diag_kernel(const int64_t *__restrict__ pairs, int n,
+                                                         int64_t *__restrict__ counts) {
+    const int i = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+    if (i < n) counts[i] = pairs[(size_t)i * n + i];
+}
+
 // PairHistogram materialisation (analysis.py:86-98): the STRICT upper triangle (i < j, the reference's
 // key order, analysis.py:70) of the n x n int64 pair counts packed row-major -- as int64 counts, or as
 // float64 count / divisor (IEEE division, correctly rounded: the value Python's int / int gives, as
@@ -2055,7 +2069,9 @@ int launch_draw(const csa_instance *I, int32_t k, uint64_t seed, uint64_t panel_
                 uint64_t *d_hashes, uint32_t *d_attempts, int32_t *d_picks, uint32_t *d_status,
                 int32_t *d_sel_out, int32_t *d_rem_out, uint64_t *d_present_out, hipStream_t stream,
                 uint16_t *d_picks_ext = nullptr, const uint64_t *d_panel_list = nullptr,
-                const unsigned long long *d_list_len = nullptr) {
+                const unsigned long long *d_list_len = nullptr, uint32_t *d_xt = nullptr,
+                int32_t *xt_written = nullptr) {
+    if (xt_written) *xt_written = 0;
     int rc = check_k(I, k);
     if (rc) return rc;
     if ((!d_panels && !d_picks_ext) || !d_status) return fail(CSA_E_INVALID, "d_panels and d_status are required");
@@ -2119,6 +2135,8 @@ int launch_draw(const csa_instance *I, int32_t k, uint64_t seed, uint64_t panel_
     A.sel_out = d_sel_out;
     A.rem_out = d_rem_out;
     A.present_out = d_present_out;
+    A.xt = nullptr;
+    A.npad = ((I->n + 255) / 256) * 256;  // csa_xt_pad
     if (d_picks_ext && !cfg.picks()) return fail(CSA_E_UNSUPPORTED, "this instance does not take the pick-list draw");
     csa_instance *M = const_cast<csa_instance *>(I);  // the lane kernel's pick-list scratch
     if (d_picks_ext)
@@ -2161,6 +2179,10 @@ int launch_draw(const csa_instance *I, int32_t k, uint64_t seed, uint64_t panel_
     if ((cfg.lane || cfg.solo) && !fused) {
         A.panels = nullptr;
         A.hashes = nullptr;
+    }
+    if (d_xt && cfg.lane && fused) {  // draw_lane_kernel's tail also writes the XT blocks
+        A.xt = d_xt;
+        if (xt_written) *xt_written = 1;
     }
     void *args[] = {&A};
     HIPCHK(hipLaunchKernel(cfg.fn, dim3((unsigned)std::max<uint64_t>(1, grid)), dim3(threads), args, lds_launch, stream));
@@ -2588,6 +2610,14 @@ int csa_pairs_pack_async(const int64_t *d_pairs, int32_t n, int32_t *d_packed, v
     return CSA_OK;
 }
 
+int csa_pairs_diag_async(const int64_t *d_pairs, int32_t n, int64_t *d_counts, void *stream) {
+    if (n <= 0 || !d_pairs || !d_counts) return fail(CSA_E_INVALID, "pairs_diag: bad arguments");
+    hipLaunchKernelGGL(pairs_diag_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, d_pairs,
+                       n, d_counts);
+    HIPCHK(hipGetLastError());
+    return CSA_OK;
+}
+
 int csa_pairs_upper_async(const int64_t *d_pairs, int32_t n, double divisor, void *d_out, void *stream) {
     if (n < 0 || (n > 1 && (!d_pairs || !d_out)) || divisor < 0.0) return fail(CSA_E_INVALID, "pairs upper: bad arguments");
     if (n < 2) return CSA_OK;
@@ -2659,6 +2689,15 @@ int csa_draw_async(const csa_instance *I, int32_t k, uint64_t seed, uint64_t pan
     if (!I) return fail(CSA_E_INVALID, "null instance");
     return launch_draw(I, k, seed, panel_begin, n_panels, max_attempts, 0, 0, d_panels, d_hashes, d_attempts,
                        d_picks, d_status, nullptr, nullptr, nullptr, (hipStream_t)stream);
+}
+
+int csa_draw_xt_async(const csa_instance *I, int32_t k, uint64_t seed, uint64_t panel_begin, uint64_t n_panels,
+                      uint32_t max_attempts, uint64_t *d_panels, uint64_t *d_hashes, uint32_t *d_attempts,
+                      uint32_t *d_status, uint32_t *d_xt, int32_t *xt_written, void *stream) {
+    if (!I || !d_xt || !xt_written) return fail(CSA_E_INVALID, "draw_xt: null instance, d_xt or xt_written");
+    return launch_draw(I, k, seed, panel_begin, n_panels, max_attempts, 0, 0, d_panels, d_hashes, d_attempts,
+                       nullptr, d_status, nullptr, nullptr, nullptr, (hipStream_t)stream, nullptr, nullptr, nullptr,
+                       d_xt, xt_written);
 }
 
 int32_t csa_picks_stride(int32_t k) { return (k + 7) & ~7; }

@@ -133,6 +133,23 @@ class DevicePipeline:
                                        N.ptr(self.attempts), None, N.ptr(self.status),
                                        _stream_ptr(stream or self.stream)))
 
+    def draw_xt(self, seed, panel_begin, S, max_attempts=0):
+        """draw() on the pipeline's stream that also writes the panels as XT into self.xt when the
+        instance takes draw_lane_kernel (csa_draw_xt_async).  Returns True when it did: the caller
+        then skips transpose_count and takes the counts from the pair diagonal (counts_from_pairs)."""
+        assert S <= self.max_panels and self.panels.numel() >= S * self.enc.W and self.want_pairs
+        written = ctypes.c_int32(0)
+        N.check(N.lib().csa_draw_xt_async(self.enc.handle, self.k, int(seed) & 0xFFFFFFFFFFFFFFFF, int(panel_begin),
+                                          int(S), max_attempts, N.ptr(self.panels), N.ptr(self.hashes),
+                                          N.ptr(self.attempts), N.ptr(self.status), N.ptr(self.xt),
+                                          ctypes.byref(written), _stream_ptr(self.stream)))
+        return bool(written.value)
+
+    def counts_from_pairs(self):
+        """self.counts = the diagonal of self.pairs (stored; after pair_counts of the whole batch)."""
+        N.check(N.lib().csa_pairs_diag_async(N.ptr(self.pairs), self.enc.n, N.ptr(self.counts),
+                                             _stream_ptr(self.stream)))
+
     def hash(self, S):
         N.check(N.lib().csa_panel_hash_async(N.ptr(self.panels), int(S), self.enc.W, N.ptr(self.hashes),
                                              _stream_ptr(self.stream)))

@@ -207,6 +207,16 @@ int csa_draw_async(const csa_instance *inst, int32_t k, uint64_t seed, uint64_t 
                    uint64_t n_panels, uint32_t max_attempts, uint64_t *d_panels,
                    uint64_t *d_hashes, uint32_t *d_attempts, int32_t *d_picks,
                    uint32_t *d_status, void *stream);
+/* csa_draw_async that also writes the launch's panels as XT (d_xt: the csa_transpose_count_async
+ * layout for n_panels, csa_xt_pad(n) persons per plane) when draw_lane_kernel runs with its fused pack
+ * (*xt_written = 1): the caller then skips csa_transpose_count_async and takes the per-person counts
+ * from the pair matrix's diagonal (csa_pairs_diag_async).  *xt_written = 0: d_xt untouched, the
+ * panels / hashes as csa_draw_async.  Replaces the separate transpose pass after one batch's draw
+ * (analysis.py:179-190 count the same panels). */
+int csa_draw_xt_async(const csa_instance *inst, int32_t k, uint64_t seed, uint64_t panel_begin,
+                      uint64_t n_panels, uint32_t max_attempts, uint64_t *d_panels, uint64_t *d_hashes,
+                      uint32_t *d_attempts, uint32_t *d_status, uint32_t *d_xt, int32_t *xt_written,
+                      void *stream);
 
 /* The same draw split in two, for instances whose batch draw is the pick-list kernel
  * (draw_lane_kernel: F <= 32, n <= 2048; csa_draw_picks_supported returns 1 for them, else 0 and
@@ -359,6 +369,10 @@ int csa_pairs_unpack_async(const int32_t *d_packed, int32_t n, int64_t *d_pairs,
  * count / divisor (IEEE, correctly rounded: Python's int / int) for divisor > 0, int64 counts for
  * divisor == 0.  Stream-ordered. */
 int csa_pairs_upper_async(const int64_t *d_pairs, int32_t n, double divisor, void *d_out, void *stream);
+
+/* Per-person counts (agent_appearance_counter, analysis.py:179, 187) = the diagonal of the n*n int64
+ * pair counts (every panel contributes x_i * x_i = x_i): d_counts[i] = d_pairs[i*n + i] (stored). */
+int csa_pairs_diag_async(const int64_t *d_pairs, int32_t n, int64_t *d_counts, void *stream);
 
 /* Decode a device status block (host copy of the 4 words) into a CSA_* code
  * and set csa_last_error() accordingly. */

@@ -54,3 +54,39 @@ def test_transpose_count_exact(gpu_available, n, S, with_xt):
     if with_xt:
         got = d_xt.cpu().numpy().view(np.uint32).reshape(nblk, 2, npad)
         assert np.array_equal(got, ref_xt)
+
+
+@pytest.mark.parametrize("name,k,S", [("sf_e_110", 110, 1), ("sf_e_110", 110, 63), ("sf_e_110", 110, 64),
+                                      ("sf_e_110", 110, 129), ("sf_e_110", 110, 20011), ("sf_e_tight_110", 110, 3001),
+                                      ("example_large_200", 200, 1000), ("synthetic8192_200", 200, 300)])
+def test_draw_xt_matches_transpose(gpu_available, name, k, S):
+    """csa_draw_xt_async: where draw_lane_kernel runs (F > 16, n <= 2048) its fused pack writes the
+    launch's XT blocks, bit-exact to csa_transpose_count_async over the same panels (npad padding words
+    zero), and the pair diagonal (csa_pairs_diag_async) equals the transpose pass's counts; elsewhere
+    it reports that it did not and leaves XT alone.  Ragged launches: 1, 63, 64, 129 panels."""
+    import torch
+    from conftest import inst_paths
+    P, Dv = pkg(), pkg("device")
+    inst = P.read_instance(*inst_paths(name), k)
+    enc = P.encode(inst.categories, inst.agents)
+    a = Dv.DevicePipeline(enc, k, S)
+    b = Dv.DevicePipeline(enc, k, S)
+    a.reset()
+    a.xt.fill_(-1)                             # every word the draw owns must be written
+    written = a.draw_xt(11, 5, S)
+    torch.cuda.synchronize()
+    lane = a.draw_kernel_name().startswith("draw_lane_kernel")
+    assert written == lane
+    b.reset()
+    b.panels.copy_(a.panels)
+    b.transpose_count(S)
+    nblk = (S + 63) // 64
+    if not written:
+        assert bool((a.xt == -1).all())
+        return
+    assert torch.equal(a.xt[: nblk * a.npad], b.xt[: nblk * b.npad])
+    a.pair_counts(S, overwrite=True, alone=True)
+    a.counts_from_pairs()
+    torch.cuda.synchronize()
+    assert torch.equal(a.counts, b.counts)
+    assert int(a.counts.sum()) == S * k
