@@ -34,6 +34,8 @@ CSA_PAIR_I8 = 1
 CSA_PAIR_OVERWRITE = 0x100  # engine flag: store this batch's pair counts instead of adding
 CSA_PAIR_SHARED = 0x200     # engine hint: the launch overlaps concurrent draws
 CSA_PAIR_ALONE = 0x400      # engine hint: nothing runs beside the launch (the kernel fastest alone)
+CSA_DRAW_RESET_STATUS = 0x1  # csa_draw_xt_async flags: zero the status words, and the draw statistics,
+CSA_DRAW_RESET_STATS = 0x2   # on the stream before the draw
 
 # every symbol include/csa_legacy.h declares, with its ctypes signature
 _P = ctypes.c_void_p
@@ -76,7 +78,7 @@ SIGNATURES = {
     "csa_pairs_unpack_async": (ctypes.c_int, [_P, _I32, _P, _P]),
     "csa_pairs_upper_async": (ctypes.c_int, [_P, _I32, ctypes.c_double, _P, _P]),
     "csa_pairs_diag_async": (ctypes.c_int, [_P, _I32, _P, _P]),
-    "csa_draw_xt_async": (ctypes.c_int, [_P, _I32, _U64, _U64, _U64, _U32, _P, _P, _P, _P, _P, _P, _P]),
+    "csa_draw_xt_async": (ctypes.c_int, [_P, _I32, _U64, _U64, _U64, _U32, _P, _P, _P, _P, _P, _P, _U32, _P]),
     "csa_status_decode": (ctypes.c_int, [_P]),
     "csa_legacy_draw_mt": (ctypes.c_int, [_I32, _I32, _I32, _P, _P, _P, _P, _P, _P, _P, _I32, _P, _U64, _U32,
                                           _I32, _P, _P, _P, _P, _P, _P, _P]),

@@ -436,9 +436,11 @@ def legacy_sample_device(enc, k, S, random_seed, keep_panels=True, chunk=1 << 20
         hashes = torch.empty(max(2 * S, 2), dtype=torch.int64, device=dev)
         pairs = torch.empty(enc.n * enc.n, dtype=torch.int64, device=dev)
         # status before the draws; the counters after the draws are enqueued (the draw stream does not
-        # wait for them, the counting on this stream does)
-        pipe.reset(pairs=False, counts=host_panels is not None)
-        if host_panels is None:
+        # wait for them, the counting on this stream does).  A one-chunk call folds the status and
+        # statistics resets into its draw call (csa_draw_xt_async).
+        one = host_panels is None and 0 < S <= C and os.environ.get("CSA_DRAW_XT", "1") != "0"
+        pipe.reset(pairs=False, counts=host_panels is not None, status=not one)
+        if host_panels is None and not one:
             reset_draw_stats(enc, pipe.stream)
         own_p, own_h, own_pairs = pipe.panels, pipe.hashes, pipe.pairs
         pipe.pairs = pairs
@@ -450,12 +452,12 @@ def legacy_sample_device(enc, k, S, random_seed, keep_panels=True, chunk=1 << 20
         table.ensure(S)
         try:
             drawn = None  # what the distinct count's side stream waits for: the draws
-            if host_panels is None and 0 < S <= C and os.environ.get("CSA_DRAW_XT", "1") != "0":
+            if one:
                 # one chunk: draw on the pipeline stream; draw_lane_kernel's fused pack also writes the XT
                 # blocks (csa_draw_xt_async), so the counting is the pair kernel alone and the counts
                 # are the pair diagonal -- the transpose pass leaves the call's serial tail
                 pipe.panels, pipe.hashes = panels[:S * W], hashes[:2 * S]
-                xt_done = pipe.draw_xt(random_seed, 0, S)
+                xt_done = pipe.draw_xt(random_seed, 0, S, reset=True)
                 drawn = torch.cuda.Event()
                 drawn.record(pipe.stream)
                 if not xt_done:

@@ -2693,8 +2693,15 @@ int csa_draw_async(const csa_instance *I, int32_t k, uint64_t seed, uint64_t pan
 
 int csa_draw_xt_async(const csa_instance *I, int32_t k, uint64_t seed, uint64_t panel_begin, uint64_t n_panels,
                       uint32_t max_attempts, uint64_t *d_panels, uint64_t *d_hashes, uint32_t *d_attempts,
-                      uint32_t *d_status, uint32_t *d_xt, int32_t *xt_written, void *stream) {
+                      uint32_t *d_status, uint32_t *d_xt, int32_t *xt_written, uint32_t flags, void *stream) {
     if (!I || !d_xt || !xt_written) return fail(CSA_E_INVALID, "draw_xt: null instance, d_xt or xt_written");
+    if ((flags & CSA_DRAW_RESET_STATUS) && d_status) HIPCHK(hipMemsetAsync(d_status, 0, 4 * sizeof(uint32_t), (hipStream_t)stream));
+    if (flags & CSA_DRAW_RESET_STATS) {  // this instance's statistics, ordered on the stream (no host wait)
+        csa_instance *M = const_cast<csa_instance *>(I);
+        ScopedDevice sd(M->device);
+        HIPCHK(hipMemsetAsync(M->d_stats, 0, 16, (hipStream_t)stream));
+        M->panels_drawn = 0;
+    }
     return launch_draw(I, k, seed, panel_begin, n_panels, max_attempts, 0, 0, d_panels, d_hashes, d_attempts,
                        nullptr, d_status, nullptr, nullptr, nullptr, (hipStream_t)stream, nullptr, nullptr, nullptr,
                        d_xt, xt_written);

@@ -211,12 +211,15 @@ int csa_draw_async(const csa_instance *inst, int32_t k, uint64_t seed, uint64_t 
  * layout for n_panels, csa_xt_pad(n) persons per plane) when draw_lane_kernel runs with its fused pack
  * (*xt_written = 1): the caller then skips csa_transpose_count_async and takes the per-person counts
  * from the pair matrix's diagonal (csa_pairs_diag_async).  *xt_written = 0: d_xt untouched, the
- * panels / hashes as csa_draw_async.  Replaces the separate transpose pass after one batch's draw
+ * panels / hashes as csa_draw_async.  flags: CSA_DRAW_RESET_STATUS / CSA_DRAW_RESET_STATS fold a
+ * batch's resets into the same call (stream-ordered before the draw).  Replaces the separate transpose pass after one batch's draw
  * (analysis.py:179-190 count the same panels). */
+#define CSA_DRAW_RESET_STATUS 0x1u /* csa_draw_xt_async flags: zero d_status (4 words) first, */
+#define CSA_DRAW_RESET_STATS 0x2u  /* and this instance's draw statistics, on the stream */
 int csa_draw_xt_async(const csa_instance *inst, int32_t k, uint64_t seed, uint64_t panel_begin,
                       uint64_t n_panels, uint32_t max_attempts, uint64_t *d_panels, uint64_t *d_hashes,
                       uint32_t *d_attempts, uint32_t *d_status, uint32_t *d_xt, int32_t *xt_written,
-                      void *stream);
+                      uint32_t flags, void *stream);
 
 /* The same draw split in two, for instances whose batch draw is the pick-list kernel
  * (draw_lane_kernel: F <= 32, n <= 2048; csa_draw_picks_supported returns 1 for them, else 0 and
