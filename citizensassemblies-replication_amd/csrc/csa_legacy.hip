@@ -2180,7 +2180,7 @@ int launch_draw(const csa_instance *I, int32_t k, uint64_t seed, uint64_t panel_
         A.panels = nullptr;
         A.hashes = nullptr;
     }
-    if (d_xt && cfg.lane && fused) {  // draw_lane_kernel's tail also writes the XT blocks
+    if (d_xt && (cfg.lane || cfg.solo) && fused) {  // the register kernels' fused tail also writes XT
         A.xt = d_xt;
         if (xt_written) *xt_written = 1;
     }

@@ -58,10 +58,11 @@ def test_transpose_count_exact(gpu_available, n, S, with_xt):
 
 @pytest.mark.parametrize("name,k,S", [("sf_e_110", 110, 1), ("sf_e_110", 110, 63), ("sf_e_110", 110, 64),
                                       ("sf_e_110", 110, 129), ("sf_e_110", 110, 20011), ("sf_e_tight_110", 110, 3001),
-                                      ("example_large_200", 200, 1000), ("synthetic8192_200", 200, 300)])
+                                      ("example_large_200", 200, 1000), ("example_large_200", 200, 257),
+                                      ("example_small_20", 20, 65), ("synthetic8192_200", 200, 300)])
 def test_draw_xt_matches_transpose(gpu_available, name, k, S):
-    """csa_draw_xt_async: where draw_lane_kernel runs (F > 16, n <= 2048) its fused pack writes the
-    launch's XT blocks, bit-exact to csa_transpose_count_async over the same panels (npad padding words
+    """csa_draw_xt_async: where a register kernel with a fused pack runs (draw_lane_kernel, F <= 32, or
+    draw_solo_kernel, F <= 16; n <= 2048) the pack also writes the launch's XT blocks, bit-exact to csa_transpose_count_async over the same panels (npad padding words
     zero), and the pair diagonal (csa_pairs_diag_async) equals the transpose pass's counts; elsewhere
     it reports that it did not and leaves XT alone.  Ragged launches: 1, 63, 64, 129 panels."""
     import torch
@@ -75,8 +76,8 @@ def test_draw_xt_matches_transpose(gpu_available, name, k, S):
     a.xt.fill_(-1)                             # every word the draw owns must be written
     written = a.draw_xt(11, 5, S)
     torch.cuda.synchronize()
-    lane = a.draw_kernel_name().startswith("draw_lane_kernel")
-    assert written == lane
+    reg = a.draw_kernel_name().startswith(("draw_lane_kernel", "draw_solo_kernel"))
+    assert written == reg
     b.reset()
     b.panels.copy_(a.panels)
     b.transpose_count(S)
