@@ -582,8 +582,10 @@ def legacy_probabilities(instance: Instance, iterations: int, random_seed: int,
 def finish(instance, enc, raw, S):
     global LAST_RUN_STATS
     LAST_RUN_STATS = raw.stats
-    # int / int true division, as the reference's count / S (one tolist, no per-element numpy indexing)
-    alloc = {aid: c / S for aid, c in zip(enc.agent_ids, np.asarray(raw.counts).tolist())}
+    # count / S as the reference's int / int true division: both operands are exact in float64 (< 2^53)
+    # and IEEE division is correctly rounded, so numpy's float64 quotient is that same value
+    alloc = dict(zip(enc.agent_ids, (np.asarray(raw.counts, dtype=np.float64) / float(S)).tolist())) if S else \
+        {aid: int(c) / S for aid, c in zip(enc.agent_ids, np.asarray(raw.counts).tolist())}
     hist = PairHistogram(len(instance.agents), counts=raw.pairs)
     hist.turn_into_probabilities_by_dividing_all_elements_by_given_number(S)
     hist._counts, hist._S = raw.pairs, S      # integer counts for stats.sorted_pair_probabilities
