@@ -348,30 +348,6 @@ def combine(counts, pairs, hashes, panels, W, exchange=None, stream=None, pair_b
     return counts, pairs, u
 
 
-def _raise_together(status, stream=None):
-    """Every rank raises when any rank's status block holds an error: all_reduce(MAX) of the error
-    code first, so no rank goes on into a collective that the failing rank never joins.  The failing
-    rank raises its own decoded error; the others the same code (KeyError for a missing candidate,
-    legacy.py:188)."""
-    import torch
-    import torch.distributed as dist
-    from . import _native as N
-    if stream is not None:
-        stream.synchronize()
-    code = status[:1].to(torch.int64)
-    _all_reduce(code, op=dist.ReduceOp.MAX)
-    c = int(code.item())
-    if not c:
-        return
-    h = status.cpu().numpy().astype(np.uint32)
-    if int(h[0]) == 0:                       # another rank failed: report its code
-        h = np.array([c, 0xFFFFFFFF, 0xFFFFFFFF, 0], np.uint32)
-    rc = N.lib().csa_status_decode(N.ptr(h))
-    if rc == N.CSA_E_NO_CANDIDATE:
-        raise KeyError("")
-    N.check(rc)
-
-
 def local_distinct_rows(hashes, panels, n, W, status=None, stream=None):
     """This rank's exact distinct panels (hash AND bitmask): (uint64 rows as an int64 tensor of
     count*W words on the inputs' device, count).  Device inputs: csa_exchange_pack_async with one
