@@ -58,6 +58,7 @@ SIGNATURES = {
     "csa_first_panel_not_in": (ctypes.c_int, [_P, _I32, _U64, _U64, _U64, _U32, _P, _U64, _U64, _P, _P]),
     "csa_draw_round_panels": (ctypes.c_int, [_P, _I32, _P]),
     "csa_draw_async": (ctypes.c_int, [_P, _I32, _U64, _U64, _U64, _U32, _P, _P, _P, _P, _P, _P]),
+    "csa_redraw_async": (ctypes.c_int, [_P, _I32, _U64, _U64, _U64, _U32, _P, _P, _P]),
     "csa_picks_stride": (_I32, [_I32]),
     "csa_draw_picks_supported": (ctypes.c_int, [_P, _I32]),
     "csa_draw_picks_async": (ctypes.c_int, [_P, _I32, _U64, _U64, _U64, _U32, _P, _P, _P, _P]),

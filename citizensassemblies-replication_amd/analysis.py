@@ -185,7 +185,8 @@ class PanelSet:
 
     ``len()`` is the device's exact distinct-panel count; iteration / membership
     decode the packed bitmasks (host array, or a device tensor copied on first
-    use) into sorted agent-id tuples, as the reference's set holds them.
+    use) into sorted agent-id tuples, as the reference's set holds them.  A
+    sharded run keeps no panels: they are re-drawn where first read (``_redraw``).
     """
 
     def __init__(self, unique_count, packed=None, n=0, agent_ids=None):
@@ -199,35 +200,34 @@ class PanelSet:
         return self._count
 
     _where = "panels were not kept; only len() is available"
-    # a sharded run gathered lazily (distributed.ShardGather): the collective that brings the ranks'
-    # distinct panels to rank 0, made only by an explicit gather() on every rank; _root: this
-    # process is rank 0
-    _source = None
-    _root = True
+    # a sharded run (distributed.PanelRedraw): nothing was kept or sent -- the job's panels are
+    # re-drawn on this process's GPU when first read, then deduplicated like kept panels
+    _redraw = None
 
-    def gather(self):
-        """The collective of a lazily gathered sharded run's found_panels (every rank calls it, in the
-        same order as the runs): the ranks' exact local distinct panels go to rank 0.  A no-op after
-        the first time and for results that were gathered already or never sharded."""
-        if self._source is not None:
-            src, self._source = self._source, None
-            p = src()
-            if self._root:
-                self._packed = p
+    def _panels(self):
+        """The kept (or re-drawn) panels, device tensor or host array; None if none were kept."""
+        if self._packed is None and self._redraw is not None:
+            self._packed, self._redraw = self._redraw(), None
+            self._check_count = True
+        return self._packed
+
+    def _distinct(self, p):
+        """Sorted distinct rows of packed panels p; a re-drawn set must have the run's exact count."""
+        if hasattr(p, "device") and not isinstance(p, np.ndarray):
+            p = p.cpu().numpy()
+        W = max((self._n + 63) // 64, 1)
+        p = np.ascontiguousarray(p).view(np.uint64).reshape(-1, W)
+        rows = np.unique(p, axis=0) if len(p) else p
+        if getattr(self, "_check_count", False) and len(rows) != self._count:
+            raise RuntimeError("found_panels: the re-drawn panels hold %d distinct panels, the run counted %d"
+                               % (len(rows), self._count))
+        return rows
 
     def _materialise(self):
-        if self._source is not None:
-            # never an implicit collective: a rank that iterates alone would wait in it forever
-            raise RuntimeError("found_panels of a sharded run were not gathered yet: call "
-                               "found_panels.gather() on every rank first (len() is already global)")
         if self._set is None:
-            if self._packed is None:
+            if self._panels() is None:
                 raise RuntimeError(self._where)
-            p = self._packed
-            if hasattr(p, "device") and not isinstance(p, np.ndarray):
-                W = (self._n + 63) // 64
-                p = p.cpu().numpy().view(np.uint64).reshape(-1, W)
-            rows = np.unique(np.ascontiguousarray(p), axis=0)
+            rows = self._distinct(self._packed)
             ids = self._ids
             self._set = {tuple(ids[q] for q in unpack_panel(r, self._n)) for r in rows}
             self._packed = None
@@ -244,12 +244,9 @@ class PanelSet:
 
     def rows(self):
         """The distinct panels as a host uint64[u, W] array (sorted rows), or None when the panels
-        were not kept (or on a rank other than 0 of a sharded run).  Device panels are copied to the
-        host here."""
-        if self._source is not None:
-            self._materialise()              # raises: not gathered yet
+        were not kept.  Device panels are copied to the host here; a sharded run's are re-drawn."""
         W = (self._n + 63) // 64
-        if self._packed is None:
+        if self._panels() is None:
             if self._set is None:
                 return None
             pos = {aid: q for q, aid in enumerate(self._ids)}
@@ -259,18 +256,14 @@ class PanelSet:
                     q = pos[aid]
                     rows[i, q >> 6] |= np.uint64(1) << np.uint64(q & 63)
             return np.unique(rows, axis=0) if len(rows) else rows
-        p = self._packed
-        if hasattr(p, "device") and not isinstance(p, np.ndarray):
-            p = p.cpu().numpy()
-        p = np.ascontiguousarray(p).view(np.uint64).reshape(-1, max(W, 1))
-        return np.unique(p, axis=0) if len(p) else p
+        self._packed = self._distinct(self._packed)   # keep the host rows (a re-draw happens once)
+        self._check_count = False
+        return self._packed
 
     # pickling (run_legacy_or_retrieve dumps the returned tuple, analysis.py:284-290): only host
     # data -- the distinct panels as packed rows (or the materialised set) -- so the pickle loads
     # on a machine without a GPU
     def __getstate__(self):
-        if self._source is not None:
-            self._materialise()              # raises: not gathered yet
         st = {"count": self._count, "n": self._n, "ids": self._ids}
         if self._set is not None:
             st["set"] = self._set
@@ -528,7 +521,7 @@ def legacy_sample_device(enc, k, S, random_seed, keep_panels=True, chunk=1 << 20
 
 def legacy_probabilities(instance: Instance, iterations: int, random_seed: int,
                          keep_panels: bool = True, rng: str = None,
-                         devices=None, gather: str = "eager") -> Tuple[ProbAllocation, PanelSet, PairHistogram]:
+                         devices=None) -> Tuple[ProbAllocation, PanelSet, PairHistogram]:
     """analysis.py:162-191 on the GPU.
 
     Returns ``({agent_id: count/S}, found_panels, pair_histogram)`` with the
@@ -545,9 +538,8 @@ def legacy_probabilities(instance: Instance, iterations: int, random_seed: int,
     ``devices`` (Philox mode, one process): shard the panels over these HIP
     devices through csa_legacy_sample_devices instead of torch.distributed.
 
-    ``gather`` (sharded runs only): "eager" gathers found_panels to rank 0 inside the call, "lazy"
-    leaves them on the ranks until every rank calls ``found_panels.gather()`` (see
-    ``distributed.legacy_probabilities_distributed``).
+    A sharded run's found_panels hold no panels: reading them on any rank re-draws the job's panels
+    on that rank's GPU (``distributed.PanelRedraw``), without a collective.
     """
     from . import distributed as D
     mode = rng or _legacy.RNG_MODE
@@ -566,8 +558,7 @@ def legacy_probabilities(instance: Instance, iterations: int, random_seed: int,
                                    host_stats=dict(zip(STAT_KEYS, (int(x) for x in st))))
         return finish(instance, enc, raw, S)
     if D.world_size() > 1:
-        return D.legacy_probabilities_distributed(instance, iterations, random_seed, keep_panels=keep_panels,
-                                                  gather=gather)
+        return D.legacy_probabilities_distributed(instance, iterations, random_seed, keep_panels=keep_panels)
     seed(random_seed)
     enc.check_quotas(instance.k)
     STREAM.take_panels(S)

@@ -2070,8 +2070,9 @@ int launch_draw(const csa_instance *I, int32_t k, uint64_t seed, uint64_t panel_
                 int32_t *d_sel_out, int32_t *d_rem_out, uint64_t *d_present_out, hipStream_t stream,
                 uint16_t *d_picks_ext = nullptr, const uint64_t *d_panel_list = nullptr,
                 const unsigned long long *d_list_len = nullptr, uint32_t *d_xt = nullptr,
-                int32_t *xt_written = nullptr) {
+                int32_t *xt_written = nullptr, bool count_stats = true) {
     if (xt_written) *xt_written = 0;
+    if (d_panel_list) count_stats = false;  // (index-list re-draws are not new panels)
     int rc = check_k(I, k);
     if (rc) return rc;
     if ((!d_panels && !d_picks_ext) || !d_status) return fail(CSA_E_INVALID, "d_panels and d_status are required");
@@ -2081,7 +2082,7 @@ int launch_draw(const csa_instance *I, int32_t k, uint64_t seed, uint64_t panel_
         for (int f = 0; f < I->F; ++f) rejected |= I->sel0[f] < I->fmin[f];
         // draw statistics as the kernels keep them: accepted new panels only (an index-list re-draw of
         // the multi-GPU owner passes its list capacity as n_panels and draws no new panel)
-        if (!rejected && !d_panel_list) const_cast<csa_instance *>(I)->panels_drawn += n_panels;
+        if (!rejected && count_stats) const_cast<csa_instance *>(I)->panels_drawn += n_panels;
         if (!d_panels) {  // pick-list draw of k = 0: nothing to write but the attempts / status
             hipLaunchKernelGGL(empty_panels_kernel, dim3((unsigned)((n_panels + 255) / 256)), dim3(256), 0, stream,
                                n_panels, d_attempts, d_status, panel_begin, rejected);
@@ -2129,7 +2130,7 @@ int launch_draw(const csa_instance *I, int32_t k, uint64_t seed, uint64_t panel_
     A.picks16 = nullptr;
     A.status = d_status;
     // legacy_find-semantics draws are counted; single attempts (csa_legacy_attempt) are not
-    A.stats = (single || d_panel_list) ? nullptr : I->d_stats;
+    A.stats = (single || !count_stats) ? nullptr : I->d_stats;
     A.panel_list = d_panel_list;   // an index list: draw_kernel GENERAL (pick_draw_config above)
     A.n_panels_dev = d_list_len;
     A.sel_out = d_sel_out;
@@ -2187,7 +2188,7 @@ int launch_draw(const csa_instance *I, int32_t k, uint64_t seed, uint64_t panel_
     void *args[] = {&A};
     HIPCHK(hipLaunchKernel(cfg.fn, dim3((unsigned)std::max<uint64_t>(1, grid)), dim3(threads), args, lds_launch, stream));
     HIPCHK(hipGetLastError());
-    if (!single && !d_panel_list) M->panels_drawn += n_panels;  // (index-list re-draws are not new panels)
+    if (!single && count_stats) M->panels_drawn += n_panels;
     if (cfg.picks() && !d_picks_ext) {  // pick lists -> packed panels (+ hashes)
         if (!fused && (rc = launch_pack(A.picks16, n_panels, k, I->W, d_panels, d_hashes, stream))) return rc;
         HIPCHK(hipEventRecord(M->picks_done, stream));
@@ -2705,6 +2706,14 @@ int csa_draw_xt_async(const csa_instance *I, int32_t k, uint64_t seed, uint64_t 
     return launch_draw(I, k, seed, panel_begin, n_panels, max_attempts, 0, 0, d_panels, d_hashes, d_attempts,
                        nullptr, d_status, nullptr, nullptr, nullptr, (hipStream_t)stream, nullptr, nullptr, nullptr,
                        d_xt, xt_written);
+}
+
+int csa_redraw_async(const csa_instance *I, int32_t k, uint64_t seed, uint64_t panel_begin, uint64_t n_panels,
+                     uint32_t max_attempts, uint64_t *d_panels, uint32_t *d_status, void *stream) {
+    if (!I || !d_panels || !d_status) return fail(CSA_E_INVALID, "redraw: null instance, d_panels or d_status");
+    return launch_draw(I, k, seed, panel_begin, n_panels, max_attempts, 0, 0, d_panels, nullptr, nullptr, nullptr,
+                       d_status, nullptr, nullptr, nullptr, (hipStream_t)stream, nullptr, nullptr, nullptr, nullptr,
+                       nullptr, /*count_stats=*/false);
 }
 
 int32_t csa_picks_stride(int32_t k) { return (k + 7) & ~7; }

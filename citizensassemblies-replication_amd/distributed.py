@@ -379,99 +379,65 @@ def local_distinct_rows(hashes, panels, n, W, status=None, stream=None):
     return send_p[: cnt * W], cnt
 
 
-GATHER_CHUNK_BYTES = 256 << 20   # rows per point-to-point message of the found_panels gather
+class PanelRedraw:
+    """found_panels of a sharded run, re-made where they are read instead of gathered.
 
+    Every panel is a pure function of (instance, k, seed, global panel index): the Philox counter
+    of each draw is (step, attempt, panel) under the key ``seed``, so the
+    panels [0, S) of the whole job -- every rank's shard -- can be drawn again on any one process.
+    Calling this re-draws them in chunks of ``chunk`` panels through ``draw(begin, count)`` (a
+    callable returning uint64[count, W]; ``device_redraw`` for the product path) into one host
+    array, with no collective: any rank may iterate, test membership or pickle its found_panels at
+    any time, alone.  The reference only ever takes len() of the set (analysis.py:575, 580) and
+    pickles it (analysis.py:290); len() needs no re-draw (the exchange's exact count)."""
 
-def _check_run_id(run_id, dev):
-    """Every rank of a gather must be gathering the same run (the ranks' n-th sharded call): an
-    all_reduce(MAX) of (id, -id) equals (id, -id) on every rank iff all ids agree; else every rank
-    raises (consistently: they all see the same reduced values), instead of rank 0 receiving
-    another run's panels."""
-    import torch
-    import torch.distributed as dist
-    t = torch.tensor([int(run_id), -int(run_id)], dtype=torch.int64, device=dev)
-    _all_reduce(t, op=dist.ReduceOp.MAX)
-    hi, lo = (int(x) for x in t.cpu().tolist())
-    if hi != int(run_id) or -lo != int(run_id):
-        raise RuntimeError("found_panels gather: the ranks are gathering different runs (run ids %d..%d; this "
-                           "rank: %d) -- gather() the sharded results in the same order on every rank"
-                           % (-lo, hi, int(run_id)))
-
-
-def gather_distinct_to_root(hashes, panels, n, W, status=None, stream=None, chunk_bytes=None, run_id=None):
-    """found_panels of a sharded run, on rank 0 only (a collective: every rank calls it): every rank
-    reduces its shard to its exact local distinct panels; one all_reduce tells rank 0 every rank's
-    count, rank 0 allocates ONE host array for all of them and receives each rank's rows straight
-    into its slice, in messages of at most ``chunk_bytes`` (no concatenated copy; over RCCL each
-    message lands in a device buffer of that size first), so no rank ever holds more than its own
-    panels on its device.  ``run_id``: checked across ranks first (_check_run_id).  Returns
-    uint64[m, W] on rank 0 (rows of all ranks; a panel drawn on two ranks appears twice and
-    PanelSet deduplicates on iteration), None elsewhere."""
-    import torch
-    import torch.distributed as dist
-    world, r = dist.get_world_size(), dist.get_rank()
-    W = int(W)
-    host = _host_collectives(hashes) or not hashes.is_cuda
-    dev = torch.device("cpu") if host else hashes.device
-    if run_id is not None:
-        _check_run_id(run_id, dev)
-    rows, cnt = local_distinct_rows(hashes, panels, n, W, status, stream)
-    counts = torch.zeros(world, dtype=torch.int64, device=dev)
-    counts[r] = cnt
-    _all_reduce(counts)
-    counts = [int(c) for c in counts.cpu().tolist()]
-    per = max(1, int(chunk_bytes or GATHER_CHUNK_BYTES) // (8 * max(W, 1)))   # rows per message
-    if r != 0:
-        src = rows.cpu() if host else rows.contiguous()
-        for o in range(0, cnt, per):
-            dist.send(src[o * W:min(cnt, o + per) * W], 0)
-        return None
-    out = np.empty((sum(counts), W), np.uint64)
-    out[:cnt] = rows.cpu().numpy().view(np.uint64).reshape(cnt, W)
-    del rows
-    buf = None if host else torch.empty(min(per, max(counts)) * W, dtype=torch.int64, device=dev)
-    at = cnt
-    for src_rank in range(1, world):
-        c = counts[src_rank]
-        for o in range(0, c, per):
-            m = min(per, c - o)
-            dst = torch.from_numpy(out[at + o:at + o + m].reshape(-1).view(np.int64))
-            if host:
-                dist.recv(dst, src_rank)                # gloo: straight into the host array
-            else:
-                dist.recv(buf[: m * W], src_rank)
-                dst.copy_(buf[: m * W])
-        at += c
-    return out
-
-
-class ShardGather:
-    """found_panels of a sharded run gathered lazily (gather="lazy"): this rank's shard (hashes and
-    panels, kept on its device until the gather) and how to gather the ranks' exact local distinct
-    panels to rank 0.  Calling it is the collective gather_distinct_to_root (every rank calls it
-    once, through PanelSet.gather(); iteration never calls it implicitly); ``run_id`` ties the
-    gather to its run on every rank."""
-
-    def __init__(self, hashes, panels, n, W, stream=None, run_id=None):
-        self.hashes, self.panels, self.n, self.W, self.stream = hashes, panels, int(n), int(W), stream
-        self.run_id = run_id
+    def __init__(self, draw, S, W, chunk=1 << 20):
+        self.draw, self.S, self.W, self.chunk = draw, int(S), int(W), max(1, int(chunk))
 
     def __call__(self):
-        out = gather_distinct_to_root(self.hashes, self.panels, self.n, self.W, stream=self.stream,
-                                      run_id=self.run_id)
-        self.hashes = self.panels = None
+        out = np.empty((self.S, max(self.W, 1)), np.uint64)
+        for off in range(0, self.S, self.chunk):
+            c = min(self.chunk, self.S - off)
+            out[off:off + c] = self.draw(off, c)
         return out
 
 
-_RUN_SEQ = [0]   # this process's sharded calls, in order (the ranks make them in the same order)
+def device_redraw(enc, k, seed, device, max_attempts=0):
+    """``draw(begin, count)`` for PanelRedraw on ``device``: csa_redraw_async (the batch draw's kernel
+    and Philox counters, not counted in the instance's draw statistics) into a device buffer, then one
+    copy to the host.  The re-drawn status block is decoded: the original call already succeeded on
+    every rank, so an error here is raised, never ignored."""
+    import torch
+    from . import _native as N
+    W = enc.W
+    seed64 = int(seed) & M64
+
+    def draw(begin, count):
+        with torch.cuda.device(device):
+            st = torch.cuda.current_stream(device)
+            buf = torch.empty(max(count * W, 1), dtype=torch.int64, device=device)
+            status = torch.zeros(4, dtype=torch.int32, device=device)
+            N.check(N.lib().csa_redraw_async(enc.handle, int(k), seed64, int(begin), int(count), int(max_attempts),
+                                             N.ptr(buf), N.ptr(status), ctypes.c_void_p(st.cuda_stream)))
+            host = buf[:count * W].cpu()
+            words = status.cpu().numpy().astype(np.uint32)
+        if words[0]:
+            _decode_status(words, int(words[0]))
+        return host.numpy().view(np.uint64).reshape(count, W)
+
+    return draw
+
+
+ERR_DRAW_PRIORITY = 1 << 16     # status codes are small; draw errors reduce above every other code
 
 
 def _decode_status(words, reduced_code):
-    """Raise the error of a status block (host uint32[4]); a rank whose own block is clean raises the
-    code another rank reported (KeyError for a missing candidate, legacy.py:188)."""
+    """Raise the error of a status block (host uint32[4]); a rank whose own block is clean -- or holds
+    another error than the one the ranks agreed on (``reduced_code``) -- raises the agreed code
+    (KeyError for a missing candidate, legacy.py:188), so every rank raises the same error."""
     from . import _native as N
     h = np.asarray(words, np.uint32)
-    if int(h[0]) == 0:
+    if int(h[0]) != int(reduced_code):
         h = np.array([reduced_code, 0xFFFFFFFF, 0xFFFFFFFF, 0], np.uint32)
     rc = N.lib().csa_status_decode(N.ptr(h))
     if rc == N.CSA_E_NO_CANDIDATE:
@@ -488,8 +454,18 @@ def _shard_exchange(enc, n_max, world, dev):
     return ex
 
 
-def legacy_probabilities_distributed(instance, iterations, random_seed, keep_panels=True, gather="eager",
-                                     chunk=None, timings=None):
+def shard_device():
+    """The GPU of this rank: LOCAL_RANK (one process per GPU, as torchrun sets it), modulo the visible
+    devices so rehearsals can put several ranks on one GPU; without LOCAL_RANK, the current device.
+    Never changes the caller's current device."""
+    import torch
+    lr = os.environ.get("LOCAL_RANK")
+    idx = int(lr) % max(torch.cuda.device_count(), 1) if lr is not None else torch.cuda.current_device()
+    return torch.device("cuda", idx)
+
+
+def legacy_probabilities_distributed(instance, iterations, random_seed, keep_panels=True, chunk=None,
+                                     timings=None):
     """analysis.py:162-191 with the panels sharded over the ranks of the default group.  Every rank
     returns the whole job's alloc, pair histogram and exact distinct-panel count.
 
@@ -499,28 +475,22 @@ def legacy_probabilities_distributed(instance, iterations, random_seed, keep_pan
     tensors (caching allocator).  Draws, counting, pairs, the draw statistics and every collective
     are stream-ordered; the host waits once, for one copy of [counts | statistics | distinct count |
     status].  The pair counts stay on the device behind the returned PairHistogram (packed and
-    divided there when first read).
+    divided there when first read).  Runs on ``shard_device()`` without changing the caller's current
+    device.
 
-    found_panels (``keep_panels``):
-      * ``gather="eager"`` (default): the ranks' exact local distinct panels are gathered to rank 0
-        inside this call (a collective every rank is already in); rank 0's set iterates like the
-        reference's, the others support len() only;
-      * ``gather="lazy"``: nothing is sent; each rank keeps its shard on its device until every rank
-        calls ``found_panels.gather()`` (the collective, checked to be the same run on all ranks).
-        Iterating, testing membership, comparing or pickling an un-gathered set raises at once on
-        any rank -- it never enters a collective by itself.
-    One rank (no exchange): no collective at all; the distinct count runs on a side stream beside the
-    last counting, and found_panels keeps the panels on the device and decodes them when iterated, as
-    the one-GPU call does (``gather`` changes nothing, ``found_panels.gather()`` is a no-op).
-    The draw statistics (analysis.LAST_RUN_STATS) are summed over ranks.  ``timings`` (a dict) gets
-    the host-side stage times in ms."""
+    found_panels: len() is the exchange's exact global count.  With more than one rank (or a forced
+    exchange) nothing else is kept and nothing is sent: iterating, ``in``, ``rows()`` or pickling on
+    ANY rank re-draws the job's panels [0, S) on that rank's GPU (PanelRedraw, csa_redraw_async) and
+    deduplicates them there -- no collective, so a rank may do it alone, at any time.  One rank (no
+    exchange): the panels of the call are the whole run's and stay on the device, decoded when read, as
+    the one-GPU call does.  ``keep_panels=False``: len() only.  The draw statistics
+    (analysis.LAST_RUN_STATS) are summed over ranks.  ``timings`` (a dict) gets the host-side stage
+    times in ms."""
     import time
     import torch
     import torch.distributed as dist
     from . import analysis as A
     from . import _native as N
-    if gather not in ("eager", "lazy"):
-        raise ValueError("gather must be 'eager' or 'lazy'")
     t0 = time.perf_counter()
     world, r = world_size(), rank()
     S = int(iterations)
@@ -532,11 +502,17 @@ def legacy_probabilities_distributed(instance, iterations, random_seed, keep_pan
     begin, end = shard_range(S, world, r)
     local = end - begin
     n_max = shard_range(S, world, 0)[1]          # rank 0 holds the largest share
-    _RUN_SEQ[0] += 1
-    run_id = _RUN_SEQ[0]
-    # one process per GPU (LOCAL_RANK); the modulo lets rehearsals put several ranks on one device
-    torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", r)) % max(torch.cuda.device_count(), 1))
-    dev = torch.device("cuda", torch.cuda.current_device())
+    dev = shard_device()
+    with torch.cuda.device(dev):
+        out = _sharded_call(A, N, dist, enc, k, S, random_seed, world, begin, local, n_max, dev, keep_panels, chunk,
+                            t0, timings, instance)
+    return out
+
+
+def _sharded_call(A, N, dist, enc, k, S, random_seed, world, begin, local, n_max, dev, keep_panels, chunk, t0, timings,
+                  instance):
+    import time
+    import torch
     C = max(1, min(max(local, 1), int(chunk or os.environ.get("CSA_SHARD_CHUNK", 1 << 20))))
     pipe = A.cached_pipeline(enc, k, C)
     # (CSA_FORCE_EXCHANGE=1: the key exchange even for one rank -- tests of its collectives on one GPU)
@@ -546,7 +522,7 @@ def legacy_probabilities_distributed(instance, iterations, random_seed, keep_pan
     st = pipe.stream
     sp = ctypes.c_void_p(st.cuda_stream)
     t1 = time.perf_counter()
-    with torch.cuda.device(dev), torch.cuda.stream(st):
+    with torch.cuda.stream(st):
         panels = torch.empty(max(local * W, 1), dtype=torch.int64, device=dev)
         hashes = torch.empty(max(2 * local, 2), dtype=torch.int64, device=dev)
         pairs = torch.empty(n * n, dtype=torch.int64, device=dev)
@@ -571,6 +547,10 @@ def legacy_probabilities_distributed(instance, iterations, random_seed, keep_pan
         # this shard's draw statistics, before the exchange's re-draws (device, no host wait)
         N.check(L.csa_instance_draw_stats_async(enc.handle, N.ptr(acc[n:n + 3]), sp))
         if ex is not None:
+            # a shard whose draw failed still enters the collectives (every rank must, or the others
+            # hang); its status block joins the MAX all_reduce below, so every rank raises the draw's
+            # error -- the exchange writes its own status only past a full segment, and the first
+            # error recorded in a block wins (csa_status_decode)
             _all_reduce_pairs(pairs, S, st)
             u = ex.run(hashes, panels, local, status=pipe.status, stream=st, panel_begin=begin,
                        redraw=(enc.handle, k, random_seed, 0))
@@ -593,7 +573,11 @@ def legacy_probabilities_distributed(instance, iterations, random_seed, keep_pan
         code = pipe.status[:1].to(torch.int64)
         if ex is not None:
             _all_reduce(acc)
+            # MAX over ranks of a priority key: a draw error (KeyError / attempt limit) on any rank
+            # outranks an exchange error on another (an overflowing segment), whatever their codes
+            code += ERR_DRAW_PRIORITY * ((code == N.CSA_E_NO_CANDIDATE) | (code == N.CSA_E_ATTEMPT_LIMIT))
             _all_reduce(code, op=dist.ReduceOp.MAX)
+            code %= ERR_DRAW_PRIORITY
         tail = torch.cat([code, pipe.status.to(torch.int64)])
         host = torch.cat([acc, tail]).cpu()          # the call's one host wait
     t2 = time.perf_counter()
@@ -603,20 +587,13 @@ def legacy_probabilities_distributed(instance, iterations, random_seed, keep_pan
     counts = h[:n].copy()
     stats = dict(zip(A.STAT_KEYS, (int(x) for x in h[n:n + 3])))
     # one rank (no exchange): its panels are the whole run's, so found_panels keeps them on the device and
-    # decodes them when iterated, as the one-GPU call does -- there is nothing to gather
+    # decodes them when iterated, as the one-GPU call does
     solo = ex is None and keep_panels
     raw = A.LegacyRaw(counts, pairs.view(n, n), int(h[n + 3]), panels[: local * W] if solo else None, None, stats)
     out = A.finish(instance, enc, raw, S)
     if keep_panels and not solo:
-        sg = ShardGather(hashes[: 2 * local], panels[: local * W], local, W, st, run_id=run_id)
-        out[1]._root = r == 0
-        out[1]._where = "found_panels of a sharded run iterate on rank 0 only (len() is global)"
-        if gather == "eager":
-            p = sg()
-            if r == 0:
-                out[1]._packed = p
-        else:
-            out[1]._source = sg
+        # nothing kept, nothing sent: the whole job's panels are re-drawn where they are read
+        out[1]._redraw = PanelRedraw(device_redraw(enc, k, random_seed, dev), S, W, chunk=max(C, 1 << 16))
     if timings is not None:
         t3 = time.perf_counter()
         timings.update(setup_ms=(t1 - t0) * 1e3, device_ms=(t2 - t1) * 1e3, finish_ms=(t3 - t2) * 1e3,

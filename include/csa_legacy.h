@@ -221,6 +221,15 @@ int csa_draw_xt_async(const csa_instance *inst, int32_t k, uint64_t seed, uint64
                       uint32_t *d_attempts, uint32_t *d_status, uint32_t *d_xt, int32_t *xt_written,
                       uint32_t flags, void *stream);
 
+/* Re-draw panels [panel_begin, panel_begin + n_panels) exactly as csa_draw_async drew them (the same
+ * kernel and Philox counters (seed, global panel index, attempt, step), so the same bitmasks), without
+ * adding them to the instance's draw statistics.  A sharded run's found_panels (analysis.py:171,186;
+ * pickled by run_legacy_or_retrieve, analysis.py:284-290) are re-made this way on whichever rank reads
+ * them, instead of being gathered from the other ranks.  d_panels: n_panels*W; d_status as above. */
+int csa_redraw_async(const csa_instance *inst, int32_t k, uint64_t seed, uint64_t panel_begin,
+                     uint64_t n_panels, uint32_t max_attempts, uint64_t *d_panels, uint32_t *d_status,
+                     void *stream);
+
 /* The same draw split in two, for instances whose batch draw is the pick-list kernel
  * (draw_lane_kernel: F <= 32, n <= 2048; csa_draw_picks_supported returns 1 for them, else 0 and
  * csa_draw_picks_async returns CSA_E_UNSUPPORTED).  csa_draw_picks_async writes each panel's k

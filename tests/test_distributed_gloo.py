@@ -10,7 +10,10 @@ csa_unique_segments_async: equal hash AND equal bitmask), all_reduce of the
 owners' counts.  The combined results must equal one unsharded run -- on an
 all-distinct instance and on a duplicate-heavy one whose duplicates land on
 different ranks -- and two different panels given the same 128-bit hash must
-still count twice (the count is exact, not hash-based).
+still count twice (the count is exact, not hash-based).  found_panels are
+re-drawn where they are read (distributed.PanelRedraw): rank 0 alone iterates
+and pickles them without entering any collective, and the pickle loads in a
+child process without a GPU.
 """
 import os
 import socket
@@ -56,52 +59,61 @@ def _worker(rank, world, port, out_dir, name):
     pairs = torch.from_numpy(coracle.pairs(panels, o.n, threads=2).ravel().copy())
     hashes = torch.from_numpy(D.panel_hashes(panels).ravel().view(np.int64).copy())
     ptens = torch.from_numpy(np.ascontiguousarray(panels).view(np.int64).ravel().copy())
-    recvs = []
-    real_recv = dist.recv
-
-    def counting_recv(tensor, src=None, *a, **kw):   # every point-to-point receive of this rank
-        recvs.append(tensor.numel())
-        return real_recv(tensor, src, *a, **kw)
-
-    dist.recv = counting_recv
     counts, pairs, u = D.combine(counts, pairs, hashes, ptens, W)
-    # found_panels as legacy_probabilities_distributed(gather="lazy") returns them: nothing gathered
-    # yet, len() global, and ANY rank that iterates / tests membership / pickles / compares before the
-    # explicit gather() raises at once -- it never enters the collective alone (no hang)
+    # found_panels as legacy_probabilities_distributed returns them on every rank: the exchange's
+    # exact count, and a PanelRedraw that re-draws the whole job [0, S) where it is read (the C oracle
+    # stands in for this rank's GPU, csa_redraw_async) -- no panels kept, nothing sent
     A = pkg("analysis")
     import pickle
     found = A.PanelSet(int(u.item()), None, o.n, list(range(o.n)))
-    found._source, found._root = D.ShardGather(hashes, ptens, e - b, W, run_id=7), rank == 0
-    assert len(found) == int(u.item()) and recvs == []
-    for touch in (lambda: sorted(found), lambda: (1,) in found, lambda: pickle.dumps(found), found.rows,
-                  lambda: found == set()):
-        with pytest.raises(RuntimeError, match="gather"):
-            touch()
-    assert recvs == []
-    D.GATHER_CHUNK_BYTES = 8 * W * 7               # 7 rows per message: several messages per rank
-    found.gather()                                 # the explicit collective, on every rank
-    if rank == 0:
-        tuples = sorted(found)
-        rows = found.rows()
-        again = pickle.loads(pickle.dumps(found))
-        assert sorted(again) == tuples and len(again) == len(found)
-        assert all(t in found for t in tuples[:5]) and (-1,) not in found
-        np.save(os.path.join(out_dir, "recvs.npy"), np.array(recvs, np.int64))
-        np.save(os.path.join(out_dir, "rows.npy"), rows)
-        np.save(os.path.join(out_dir, "counts.npy"), counts.numpy())
-        np.save(os.path.join(out_dir, "pairs.npy"), pairs.numpy())
-        np.save(os.path.join(out_dir, "unique.npy"), np.array([int(u.item())]))
-    else:
-        with pytest.raises(RuntimeError):
-            iter(found)
-        assert recvs == []
-    # ranks gathering DIFFERENT runs (ids 10 / 11): every rank raises, rank 0 receives nothing
-    other = A.PanelSet(int(u.item()), None, o.n, list(range(o.n)))
-    other._source, other._root = D.ShardGather(hashes, ptens, e - b, W, run_id=10 + rank), rank == 0
-    n_recv = len(recvs)
-    with pytest.raises(RuntimeError, match="different runs"):
-        other.gather()
-    assert len(recvs) == n_recv
+
+    def redraw(b_, c_):
+        rc_, p_, _, _ = coracle.draw(o, K, SEED, b_, c_, threads=2)
+        assert rc_ == 0
+        return p_
+
+    found._redraw = D.PanelRedraw(redraw, S, W, chunk=777)      # several chunks, a ragged last one
+    assert len(found) == int(u.item())
+    dist.barrier()
+    # every collective / point-to-point entry of torch.distributed is counted from here on
+    entered = []
+    names = ("send", "recv", "isend", "irecv", "all_reduce", "all_gather", "all_to_all_single", "broadcast",
+             "gather", "scatter", "reduce", "barrier", "all_gather_object", "gather_object", "broadcast_object_list")
+    real = {nm: getattr(dist, nm) for nm in names}
+
+    def spy(nm):
+        def f(*a, **kw):
+            entered.append(nm)
+            return real[nm](*a, **kw)
+        return f
+
+    for nm in names:
+        setattr(dist, nm, spy(nm))
+    try:
+        if rank == 0:   # rank 0 ALONE reads its found_panels, while the other ranks are elsewhere
+            tuples = sorted(found)
+            rows = found.rows()
+            blob = pickle.dumps(found)
+            assert all(t in found for t in tuples[:5]) and (-1,) not in found
+            assert entered == []
+            np.save(os.path.join(out_dir, "rows.npy"), rows)
+            np.save(os.path.join(out_dir, "counts.npy"), counts.numpy())
+            np.save(os.path.join(out_dir, "pairs.npy"), pairs.numpy())
+            np.save(os.path.join(out_dir, "unique.npy"), np.array([int(u.item())]))
+            with open(os.path.join(out_dir, "found.pkl"), "wb") as f:
+                f.write(blob)
+            with open(os.path.join(out_dir, "tuples.txt"), "w") as f:
+                f.write(repr(tuples))
+        else:
+            assert entered == []
+    finally:
+        for nm in names:
+            setattr(dist, nm, real[nm])
+    # a forged count: the re-drawn set must have the run's exact count, or reading it raises
+    bad = A.PanelSet(int(u.item()) + 1, None, o.n, list(range(o.n)))
+    bad._redraw = D.PanelRedraw(redraw, S, W, chunk=4096)
+    with pytest.raises(RuntimeError, match="re-drawn"):
+        bad.rows()
     dist.barrier()
     dist.destroy_process_group()
 
@@ -124,12 +136,20 @@ def test_gloo_exchange_matches_single_run(tmp_path, world, name):
         # duplicates really are split across ranks: every shard holds most of the 100 panels
         assert want == 100
     assert int(np.load(tmp_path / "unique.npy")[0]) == want
-    # the rows gathered on rank 0 (each rank's local distinct set) are exactly the distinct panels
-    # (PanelSet.rows deduplicates), received in messages of <= 7 rows, none before iteration
+    # the panels rank 0 re-drew alone are exactly the distinct panels of the single run
     rows = np.load(tmp_path / "rows.npy")
     assert np.array_equal(rows, np.unique(panels, axis=0))
-    recvs = np.load(tmp_path / "recvs.npy")
-    assert len(recvs) >= world - 1 and recvs.max() <= 7 * panels.shape[1]
+    # rank 0's pickle loads and iterates in a child process that has no GPU at all
+    import subprocess
+    import sys
+    env = dict(os.environ, HIP_VISIBLE_DEVICES="-1", CUDA_VISIBLE_DEVICES="-1", ROCR_VISIBLE_DEVICES="-1")
+    code = ("import pickle, sys; sys.path.insert(0, %r); import torch; assert not torch.cuda.is_available(); "
+            "f = pickle.load(open(%r, 'rb')); print(repr(sorted(f))); print(len(f))"
+            % (REPO, str(tmp_path / "found.pkl")))
+    out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr
+    got, ln = out.stdout.strip().splitlines()
+    assert got == (tmp_path / "tuples.txt").read_text() and int(ln) == want
 
 
 def _collision_worker(rank, world, port, out_dir):

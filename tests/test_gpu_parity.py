@@ -7,6 +7,7 @@ met with equality).
 """
 import ctypes
 import hashlib
+import os
 
 import numpy as np
 import pytest
@@ -471,20 +472,44 @@ def test_combine_rccl_world1(gpu_available):
     assert int(u.item()) == S      # sf_e_110 at 2e4 panels: all distinct
 
 
+def _rccl_world1():
+    import socket
+    import torch.distributed as dist
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    dist.init_process_group("nccl", init_method="tcp://127.0.0.1:%d" % port, rank=0, world_size=1)
+
+
+def _load_in_cpu_child(path):
+    """sorted(found_panels) and len() of a pickled result, loaded in a child process with no GPU."""
+    import subprocess
+    import sys
+    from conftest import REPO
+    env = dict(os.environ, HIP_VISIBLE_DEVICES="-1", CUDA_VISIBLE_DEVICES="-1", ROCR_VISIBLE_DEVICES="-1")
+    code = ("import pickle, sys; sys.path.insert(0, %r); import torch; assert not torch.cuda.is_available(); "
+            "a, f, h = pickle.load(open(%r, 'rb')); print(repr(sorted(f))); print(len(f))" % (REPO, str(path)))
+    out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr
+    got, ln = out.stdout.strip().splitlines()
+    return got, int(ln)
+
+
 @pytest.mark.parametrize("name,k,S,chunk", [("sf_e_110", 110, 30001, 7000),
                                             ("couples_panel_from_twenty_people_no_constraints_2", 2, 20000, 0),
                                             ("synthetic8192_200", 200, 3000, 1000)])
 @pytest.mark.parametrize("force_exchange", ["0", "1"])
-def test_distributed_call_rccl_world1(gpu_available, monkeypatch, name, k, S, chunk, force_exchange):
+def test_distributed_call_rccl_world1(gpu_available, monkeypatch, tmp_path, name, k, S, chunk, force_exchange):
     """legacy_probabilities_distributed over a one-rank RCCL group (the product path's own
     collectives: packed pair all_reduce, the 24-byte key exchange, one all_reduce of counts +
     statistics + distinct count): equal to legacy_probabilities on one GPU -- alloc, pair values,
-    distinct count, draw statistics, found_panels (eager gather) -- on the first call and on a
-    second call that reuses the cached pipeline and exchange; with the exchange, lazy found_panels
-    fail fast before gather() and equal after it; without it (one rank, CSA_FORCE_EXCHANGE=0) there
-    is nothing to gather: found_panels stay on the device, pickle at once, and gather() is a no-op."""
+    distinct count, draw statistics, found_panels -- on the first call and on a second call that
+    reuses the cached pipeline and exchange.  With the exchange, found_panels keep nothing: reading
+    them re-draws the job on this GPU (csa_redraw_async) without a collective, the re-draw leaves the
+    instance's draw statistics alone, and the pickle loads in a process without a GPU.  The call
+    leaves the caller's current device as it found it."""
     import pickle
-    import socket
+    import torch
     import torch.distributed as dist
     A = pkg("analysis")
     Dd = pkg("distributed")
@@ -495,28 +520,121 @@ def test_distributed_call_rccl_world1(gpu_available, monkeypatch, name, k, S, ch
     alloc, found, hist = A.legacy_probabilities(inst, S, 9)
     stats = dict(A.LAST_RUN_STATS)
     want_up, want_found = np.array(hist.upper()), sorted(found)
-    with socket.socket() as sk:
-        sk.bind(("127.0.0.1", 0))
-        port = sk.getsockname()[1]
-    dist.init_process_group("nccl", init_method="tcp://127.0.0.1:%d" % port, rank=0, world_size=1)
+    dev0 = torch.cuda.current_device()
+    _rccl_world1()
     try:
         for call in range(2):
             tm = {}
             a2, f2, h2 = Dd.legacy_probabilities_distributed(inst, S, 9, timings=tm)
+            assert torch.cuda.current_device() == dev0
             assert a2 == alloc and len(f2) == len(found) and A.LAST_RUN_STATS == stats
             assert np.array_equal(h2.upper(), want_up)
+            if force_exchange == "1":
+                assert f2._redraw is not None and f2._packed is None      # nothing kept, nothing sent
+            enc = A.encode_cached(inst.categories, inst.agents)
+            before = A.draw_stats(enc)
             assert sorted(f2) == want_found
+            assert A.draw_stats(enc) == before          # the re-draw is not counted as new draws
             assert tm["total_ms"] > 0
-        a3, f3, h3 = Dd.legacy_probabilities_distributed(inst, S, 9, gather="lazy")
-        if force_exchange == "1":
-            with pytest.raises(RuntimeError, match="gather"):
-                pickle.dumps(f3)
-        else:
-            assert sorted(pickle.loads(pickle.dumps(f3))) == want_found
-        f3.gather()
-        assert sorted(f3) == want_found and a3 == alloc
+        a3, f3, h3 = Dd.legacy_probabilities_distributed(inst, S, 9)
+        with open(tmp_path / "r.pkl", "wb") as f:
+            pickle.dump((a3, f3, h3), f)
+        got, ln = _load_in_cpu_child(tmp_path / "r.pkl")
+        assert got == repr(want_found) and ln == len(found)
+        a4, f4, _ = Dd.legacy_probabilities_distributed(inst, S, 9, keep_panels=False)
+        assert len(f4) == len(found)
+        with pytest.raises(RuntimeError, match="not kept"):
+            sorted(f4)
     finally:
         dist.destroy_process_group()
+
+
+def _no_candidate_instance():
+    """n = k = 102, one feature with min 0: every panel raises KeyError at step 101 (legacy.py:188)."""
+    cats = {"c": {"f": {"min": 0, "max": 200, "selected": 0, "remaining": 102}}}
+    return pkg().Instance(k=102, categories=cats, agents={i: {"c": "f"} for i in range(102)})
+
+
+def _feasible_102(k):
+    """The same pool shape (n = 102, W = 2, one category) split over two features: every draw succeeds."""
+    cats = {"c": {"f": {"min": 0, "max": 200, "selected": 0, "remaining": 51},
+                  "g": {"min": 0, "max": 200, "selected": 0, "remaining": 51}}}
+    return pkg().Instance(k=k, categories=cats, agents={i: {"c": "fg"[i % 2]} for i in range(102)})
+
+
+def test_distributed_no_candidate_rccl_world1(gpu_available, monkeypatch):
+    """The sharded call's failure path under a one-rank RCCL group with the exchange forced on: a
+    shard whose every draw raised still enters the pair all_reduce and the key exchange (on its
+    unwritten panels), and the call raises KeyError, as the one-GPU call (legacy.py:188)."""
+    Dd = pkg("distributed")
+    import torch.distributed as dist
+    monkeypatch.setenv("CSA_FORCE_EXCHANGE", "1")
+    _rccl_world1()
+    try:
+        for S in (10, 5000):
+            with pytest.raises(KeyError):
+                Dd.legacy_probabilities_distributed(_no_candidate_instance(), S, 0)
+        # the next call on the same group is unaffected
+        a, f, _ = Dd.legacy_probabilities_distributed(_feasible_102(20), 300, 1)
+        assert abs(sum(a.values()) - 20) < 1e-9 and len(f) > 1
+    finally:
+        dist.destroy_process_group()
+
+
+def _fail_worker(rank, world, port, out_dir):
+    import os
+    import sys
+    import torch.distributed as dist
+    from conftest import REPO
+    sys.path.insert(0, REPO)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        Dd = pkg("distributed")
+        # rank 0: a feasible instance whose exchange overflows its (forced tiny) segments -- an
+        # exchange error, CSA_E_UNSUPPORTED (5); rank 1: every draw raises KeyError, CSA_E_NO_CANDIDATE
+        # (3).  The collectives have the same sizes (n = 102 on both).  Every rank must raise the DRAW
+        # error: a MAX of the raw codes would hand rank 0 the exchange's instead
+        Dd.exchange_capacity = lambda n_local, world_: 1
+        own = []
+        real_decode = Dd._decode_status
+
+        def decode(words, reduced):          # this rank's own status code, then the agreed one
+            own.append((int(words[0]), int(reduced)))
+            return real_decode(words, reduced)
+
+        Dd._decode_status = decode
+        inst = _feasible_102(20) if rank == 0 else _no_candidate_instance()
+        try:
+            Dd.legacy_probabilities_distributed(inst, 4000, 0)
+            outcome = "ok"
+        except KeyError:
+            outcome = "KeyError"
+        except Exception as e:      # noqa: BLE001
+            outcome = "%s: %s" % (type(e).__name__, e)
+        outcome += " own=%d agreed=%d" % own[0] if own else " (no status decoded)"
+        with open(os.path.join(out_dir, "rank%d.txt" % rank), "w") as f:
+            f.write(outcome)
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_distributed_draw_error_outranks_exchange_error(gpu_available, tmp_path):
+    """Two ranks (gloo, one GPU): a draw error on one rank and an exchange error on the other -> every
+    rank raises KeyError (the exchange's status never masks the draw's)."""
+    import socket
+    import torch.multiprocessing as mp
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    mp.spawn(_fail_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True)
+    N = pkg("_native")
+    # rank 0's own block held the exchange's overflow, rank 1's the draw's KeyError; both raise KeyError
+    assert [(tmp_path / ("rank%d.txt" % r)).read_text() for r in range(2)] == [
+        "KeyError own=%d agreed=%d" % (N.CSA_E_UNSUPPORTED, N.CSA_E_NO_CANDIDATE),
+        "KeyError own=%d agreed=%d" % (N.CSA_E_NO_CANDIDATE, N.CSA_E_NO_CANDIDATE)]
 
 
 @pytest.mark.parametrize("name,k,S", [("couples_panel_from_twenty_people_no_constraints_2", 2, 300000),
@@ -543,7 +661,7 @@ def test_unique_partitioned_matches_oracle(gpu_available, name, k, S):
     assert got["1"] == got["0"] == want
 
 
-def _dist_worker(rank, world, port, out_dir, name, k, S, seed, mode):
+def _dist_worker(rank, world, port, out_dir, name, k, S, seed):
     import os
     import sys
     import torch.distributed as dist
@@ -556,56 +674,46 @@ def _dist_worker(rank, world, port, out_dir, name, k, S, seed, mode):
         import pickle
         A = pkg("analysis")
         inst = pkg().read_instance(*inst_paths(name), k)
-        recvs = []
-        real_recv = dist.recv
-
-        def counting_recv(tensor, src=None, *a, **kw):
-            recvs.append(int(tensor.numel()))
-            return real_recv(tensor, src, *a, **kw)
-
-        dist.recv = counting_recv
-        alloc, found, hist = A.legacy_probabilities(inst, S, seed, gather=mode)      # world > 1: sharded
-        if mode == "lazy":
-            assert recvs == []             # nothing sent until the explicit gather
-            with pytest.raises(RuntimeError, match="gather"):
-                sorted(found)              # fails at once on any rank, never waits in a collective
-            with pytest.raises(RuntimeError, match="gather"):
-                pickle.dumps((alloc, found, hist))
-            assert recvs == []
-            found.gather()                 # the collective, every rank
-        assert bool(recvs) == (rank == 0)  # eager: gathered inside the call
-        if rank == world - 1:
-            np.save(os.path.join(out_dir, "unique_last.npy"), np.array([len(found)]))
-        if rank == 0:           # found_panels iterate on rank 0 (the ranks' distinct panels gathered)
+        alloc, found, hist = A.legacy_probabilities(inst, S, seed)      # world > 1: sharded
+        dist.barrier()
+        entered = []
+        names = ("send", "recv", "isend", "irecv", "all_reduce", "all_gather", "all_to_all_single", "broadcast",
+                 "barrier")
+        real = {nm: getattr(dist, nm) for nm in names}
+        for nm in names:
+            setattr(dist, nm, (lambda nm_: lambda *a, **kw: (entered.append(nm_), real[nm_](*a, **kw))[1])(nm))
+        try:
+            # the LAST rank reads its found_panels alone (re-drawn on its GPU), no collective entered
+            if rank == world - 1:
+                tuples = sorted(found)
+                assert all(t in found for t in tuples[:3])
+                np.save(os.path.join(out_dir, "found.npy"), np.array(tuples))
+                with open(os.path.join(out_dir, "result.pkl"), "wb") as f:
+                    pickle.dump((alloc, found, hist), f)
+            assert entered == []
+        finally:
+            for nm in names:
+                setattr(dist, nm, real[nm])
+        if rank == 0:
             np.save(os.path.join(out_dir, "alloc.npy"), np.array([alloc[i] for i in range(len(alloc))]))
             np.save(os.path.join(out_dir, "upper.npy"), hist.upper())
             np.save(os.path.join(out_dir, "unique.npy"), np.array([len(found)]))
-            tuples = sorted(found)
-            assert all(t in found for t in tuples[:3])
-            np.save(os.path.join(out_dir, "found.npy"), np.array(tuples))
-            with open(os.path.join(out_dir, "result.pkl"), "wb") as f:
-                pickle.dump((alloc, found, hist), f)
-        else:
-            with pytest.raises(RuntimeError):
-                iter(found)                # len() only on the other ranks
-            pickle.dumps((alloc, found, hist))   # holds the count, no collective
         dist.barrier()
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("name,k,S,seed,chunk,mode", [("sf_e_110", 110, 9001, 3, 0, "eager"),
-                                                      ("sf_e_110", 110, 9001, 4, 1700, "lazy"),
-                                                      ("couples_panel_from_twenty_people_no_constraints_2", 2, 5000, 1,
-                                                       0, "eager"),
-                                                      ("couples_panel_from_twenty_people_no_constraints_2", 2, 5000, 2,
-                                                       700, "lazy")])
-def test_legacy_probabilities_distributed_gloo(gpu_available, tmp_path, monkeypatch, name, k, S, seed, chunk, mode):
+@pytest.mark.parametrize("name,k,S,seed,chunk", [("sf_e_110", 110, 9001, 3, 0),
+                                                 ("sf_e_110", 110, 9001, 4, 1700),
+                                                 ("couples_panel_from_twenty_people_no_constraints_2", 2, 5000, 1, 0),
+                                                 ("couples_panel_from_twenty_people_no_constraints_2", 2, 5000, 2,
+                                                  700)])
+def test_legacy_probabilities_distributed_gloo(gpu_available, tmp_path, monkeypatch, name, k, S, seed, chunk):
     """analysis.legacy_probabilities with a 2-rank process group (both ranks on this GPU, gloo:
     RCCL refuses two ranks on one device): the sharded draw (``chunk``: each rank's shard drawn in
-    chunks of that many panels, counted beside the next chunk's draw), the exact panel exchange and the
-    found_panels -- gathered to rank 0 inside the call (eager) or by the explicit gather() (lazy, which
-    fails fast when touched before it) -- `in`, and the pickled tuple equal the single-GPU result."""
+    chunks of that many panels, counted beside the next chunk's draw), the exact panel exchange, and
+    found_panels re-drawn by one rank alone (no collective) -- `in`, and the pickled tuple (loaded in
+    a process without a GPU) equal the single-GPU result."""
     import socket
     import torch.multiprocessing as mp
     A = pkg("analysis")
@@ -614,19 +722,16 @@ def test_legacy_probabilities_distributed_gloo(gpu_available, tmp_path, monkeypa
     with socket.socket() as sk:
         sk.bind(("127.0.0.1", 0))
         port = sk.getsockname()[1]
-    mp.spawn(_dist_worker, args=(2, port, str(tmp_path), name, k, S, seed, mode), nprocs=2, join=True)
+    mp.spawn(_dist_worker, args=(2, port, str(tmp_path), name, k, S, seed), nprocs=2, join=True)
     inst = pkg().read_instance(*inst_paths(name), k)
     alloc, found, hist = A.legacy_probabilities(inst, S, seed)
     assert np.load(tmp_path / "alloc.npy").tolist() == [alloc[i] for i in range(len(alloc))]
     assert np.array_equal(np.load(tmp_path / "upper.npy"), hist.upper())
     assert int(np.load(tmp_path / "unique.npy")[0]) == len(found)
-    assert int(np.load(tmp_path / "unique_last.npy")[0]) == len(found)
     assert np.load(tmp_path / "found.npy").tolist() == [list(p) for p in sorted(found)]
     assert A.LAST_RUN_STATS["attempts"] >= S
-    import pickle
-    with open(tmp_path / "result.pkl", "rb") as f:
-        _, found_p, _ = pickle.load(f)
-    assert sorted(found_p) == sorted(found) and len(found_p) == len(found)
+    got, ln = _load_in_cpu_child(tmp_path / "result.pkl")
+    assert got == repr(sorted(found)) and ln == len(found)
 
 
 def test_n16384_boundary(gpu_available):
