@@ -72,6 +72,11 @@ def parse():
                     help="where pick lists become panels: inside the draw kernel (fused, default), "
                          "picks_pack_kernel after the draw on the draw stream, or first on the counting "
                          "stream (one pick-list buffer per panel buffer)")
+    ap.add_argument("--xt-from", default="draw", choices=("draw", "count"),
+                    help="where the pair kernel's XT operand comes from: the draw kernel's fused pack "
+                         "(csa_draw_xt_async, one XT buffer per panel buffer; the counts are then the pair "
+                         "matrix's diagonal) where the instance's draw kernel has one, else -- or with "
+                         "'count' -- xt_count_kernel on the counting stream")
     ap.add_argument("--iso-steps", type=int, default=2,
                     help="serial steps after the timed region that measure each kernel alone (not in `value`)")
     ap.add_argument("--exchange", default="keys", choices=("keys", "bitmask"),
@@ -489,6 +494,11 @@ def main():
     hbufs = [pipe.hashes] + [torch.empty_like(pipe.hashes) for _ in range(nb - 1)]
     pack_on_count = split and args.pack_on == "count"
     kbufs = ([pipe.picks] + [torch.empty_like(pipe.picks) for _ in range(nb - 1)]) if pack_on_count else None
+    # XT from the draw (the register kernels' fused pack): one XT buffer per panel buffer, since the next
+    # draws write theirs while this step's pair kernel reads
+    xt_draw = want_pairs and not split and args.xt_from == "draw" and draw_name.startswith(("draw_lane", "draw_solo"))
+    xbufs = ([pipe.xt] + [torch.empty_like(pipe.xt) for _ in range(nb - 1)]) if xt_draw else None
+    fused_xt = [False] * nb      # did the draw of buffer b write its XT
     drawn = [torch.cuda.Event() for _ in range(nb)]    # draw + pack of the buffer finished (draw stream)
     counted = [torch.cuda.Event() for _ in range(nb)]  # counting of the buffer finished (counting stream)
     stages = ["draw", "pack", "xt_count", "pairs", "unique", "exchange"]
@@ -518,6 +528,11 @@ def main():
                 e[1].record(ds)
             if not pack_on_count:
                 pipe.pack(S, stream=ds)
+        elif xt_draw:
+            pipe.xt = xbufs[b]
+            fused_xt[b] = pipe.draw_xt(args.seed, begin, S, stream=ds)
+            if e:
+                e[1].record(ds)
         else:
             pipe.draw(args.seed, begin, S, stream=ds)
             if e:
@@ -542,7 +557,10 @@ def main():
                 rec[j]["pack"] = (e[5], e[0])
         if e:
             e[0].record(stream)
-        pipe.transpose_count(S)
+        if xt_draw:
+            pipe.xt = xbufs[b]
+        if not fused_xt[b]:
+            pipe.transpose_count(S)
         if e:
             e[1].record(stream)
         if want_pairs:
@@ -550,6 +568,8 @@ def main():
             # next steps in flight on the other stream the per-CU pair kernel takes its 256-register
             # form, which leaves room for a draw workgroup beside it
             pipe.pair_counts(S, overwrite=True, shared=overlap)
+            if fused_xt[b]:
+                pipe.counts_from_pairs()     # the step's counts: the stored pair matrix's diagonal
         if e:
             e[2].record(stream)
         if world == 1:
@@ -665,6 +685,8 @@ def main():
     npad = pipe.npad
     nblk = (S + 63) // 64
     draw_bytes = S * 2 * k if split else S * (8 * W + 16)   # pick lists written (or bitmasks + hashes)
+    if any(fused_xt):
+        draw_bytes += ((S + 63) // 64) * pipe.npad * 8    # + the XT operand it writes (fused pack)
     pack_bytes = S * (2 * k + 8 * W + 16)                  # read the pick lists, write panels + hashes
     xt_bytes = S * 8 * W + nblk * npad * 8 + n * 8         # read panels, write transposed bits + counts
     pair_ops = S * n * (n + 1)                             # triangle form of 2*S*n^2
@@ -777,7 +799,9 @@ def main():
             args.config, S, k, n, enc.C, enc.F, "pairs+" if want_pairs else ""),
             "panels_per_gpu_per_step": S, "instance": inst_dir, "parallelism": "panel shards x%d" % world,
             "pipeline": ("draws on their own stream, %d steps ahead of the counting%s" % (
-                ahead, " and the exchange" if world > 1 else "")) if overlap else "serial"},
+                ahead, " and the exchange" if world > 1 else "")) if overlap else "serial",
+            "xt_operand": ("written by the draw kernel's fused pack (one XT buffer per panel buffer); counts = "
+                           "the stored pair matrix's diagonal") if any(fused_xt) else "xt_count_kernel"},
         "roofline": roof,
         "kernels": kernels,
         "kernel_timing": kernel_timing,

@@ -35,6 +35,15 @@ def __getattr__(name):           # analysis.RNG_MODE follows legacy.RNG_MODE (se
 ProbAllocation = Dict
 
 
+def _divide(u, d):
+    """u / d as the reference's `/` on every value (analysis.py:86-88): numpy true division, except
+    integer counts over an int that float64 cannot hold exactly, which Python divides exactly
+    (int / int is correctly rounded; numpy would round the divisor first)."""
+    if u.dtype.kind in "iu" and isinstance(d, (int, np.integer)) and not isinstance(d, bool) and float(d) != d:
+        return np.array([x / int(d) for x in u.tolist()], np.float64)
+    return u / d
+
+
 class PairHistogram:
     """analysis.py:68-98 with a packed backing store.
 
@@ -77,12 +86,15 @@ class PairHistogram:
         import torch
         src, n = self._src, self.n
         m = n * (n - 1) // 2
-        div = float(self._divs[0]) if self._divs else 0.0
-        rest = self._divs[1:] if self._divs else []
-        dt = torch.float64 if div > 0.0 else torch.int64
-        if div > 0.0 and float(self._divs[0]) != self._divs[0]:
-            div = 0.0                                   # a divisor that is not exact in float64: host division
-            rest, dt = self._divs, torch.int64
+        # the device divides only by a first divisor that is positive and exact in float64 (S, as
+        # legacy_probabilities passes it); any other divisor -- negative, fractional types, huge ints --
+        # is applied on the host, in order, as numpy true division
+        d0 = self._divs[0] if self._divs else None
+        on_device = d0 is not None and isinstance(d0, (int, float, np.integer, np.floating)) and \
+            not isinstance(d0, bool) and float(d0) > 0.0 and float(d0) == d0
+        div = float(d0) if on_device else 0.0
+        rest = self._divs[1:] if on_device else list(self._divs)
+        dt = torch.float64 if on_device else torch.int64
         dev = src.device
         with torch.cuda.device(dev):
             st = torch.cuda.current_stream(dev)
@@ -93,7 +105,7 @@ class PairHistogram:
             st.synchronize()
         u = h.numpy()[:m]
         for dv in rest:
-            u = u / dv
+            u = _divide(u, dv)
         return u
 
     @property
@@ -102,7 +114,7 @@ class PairHistogram:
             if isinstance(self._src, np.ndarray):
                 u = self._src[np.triu_indices(self.n, 1)]
                 for d in self._divs:
-                    u = u / d
+                    u = _divide(u, d)
             else:
                 u = self._materialise_device()
             self._uv, self._src, self._divs = u, None, []
@@ -141,10 +153,14 @@ class PairHistogram:
         self._writable(isinstance(value, float))[self._index(i, j)] = value
 
     def turn_into_probabilities_by_dividing_all_elements_by_given_number(self, num):
+        # analysis.py:86-88 divides every value with Python's `/`: a zero divisor raises
+        # ZeroDivisionError at once (for int and float values alike) when there is any pair
+        if num == 0 and len(self):
+            raise ZeroDivisionError("division by zero")
         if self._uv is None:
             self._divs.append(num)
         else:
-            self._u = self._uv / num
+            self._u = _divide(self._uv, num)
         self._counts = self._S = None
 
     def add_portfolio_of_panels_to_histogram(self, portfolio, probabilities):

@@ -133,12 +133,14 @@ class DevicePipeline:
                                        N.ptr(self.attempts), None, N.ptr(self.status),
                                        _stream_ptr(stream or self.stream)))
 
-    def draw_xt(self, seed, panel_begin, S, max_attempts=0, reset=False):
-        """draw() on the pipeline's stream that also writes the panels as XT into self.xt when the
-        instance takes draw_lane_kernel (csa_draw_xt_async).  Returns True when it did: the caller
-        then skips transpose_count and takes the counts from the pair diagonal (counts_from_pairs).
-        ``reset``: the status words and the instance's draw statistics are zeroed first, in the same
-        call (stream-ordered)."""
+    def draw_xt(self, seed, panel_begin, S, max_attempts=0, reset=False, stream=None):
+        """draw() on ``stream`` (default: the pipeline's stream) that also writes the panels as XT into
+        self.xt when the instance takes a register kernel with a fused pack (draw_lane_kernel /
+        draw_solo_kernel; csa_draw_xt_async).  Returns True when it did: the caller then skips
+        transpose_count and takes the counts from the pair diagonal (counts_from_pairs).  ``reset``: the
+        status words and the instance's draw statistics are zeroed first, in the same call
+        (stream-ordered).  A caller that overlaps draws with counting swaps ``self.xt`` between
+        buffers like ``self.panels`` (bench.py)."""
         assert S <= self.max_panels and self.panels.numel() >= S * self.enc.W and self.want_pairs
         written = ctypes.c_int32(0)
         N.check(N.lib().csa_draw_xt_async(self.enc.handle, self.k, int(seed) & 0xFFFFFFFFFFFFFFFF, int(panel_begin),
@@ -146,7 +148,7 @@ class DevicePipeline:
                                           N.ptr(self.attempts), N.ptr(self.status), N.ptr(self.xt),
                                           ctypes.byref(written),
                                           (N.CSA_DRAW_RESET_STATUS | N.CSA_DRAW_RESET_STATS) if reset else 0,
-                                          _stream_ptr(self.stream)))
+                                          _stream_ptr(stream or self.stream)))
         return bool(written.value)
 
     def counts_from_pairs(self):

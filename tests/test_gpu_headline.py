@@ -129,3 +129,25 @@ def test_growing_calls_reallocate_table_on_side_stream(gpu_available):
         assert [alloc[i] for i in range(len(alloc))] == (coracle.counts(opanels, o.n) / S).tolist(), S
         del opanels
     assert all(b > a for a, b in zip(slots, slots[1:])), slots      # the table really grew every call
+
+
+def test_device_histogram_divisors(gpu_available):
+    """a PairHistogram over device counts divides like the reference for any divisor --
+    only a positive divisor exact in float64 goes to the device (csa_pairs_upper_async), a negative or
+    huge one is applied on the host, and zero raises ZeroDivisionError (analysis.py:86-88)."""
+    import torch
+    A = pkg("analysis")
+    n = 37
+    m = np.random.default_rng(5).integers(0, 1000, size=(n, n)).astype(np.int64)
+    iu = np.triu_indices(n, 1)
+    for divs in ([7], [-3], [-3, 7], [10 ** 30], [7, 10 ** 30], [2.5]):
+        h = A.PairHistogram(n, counts=torch.from_numpy(m).cuda())
+        for d in divs:
+            h.turn_into_probabilities_by_dividing_all_elements_by_given_number(d)
+        want = [int(x) for x in m[iu]]
+        for d in divs:
+            want = [x / d for x in want]
+        assert h.upper().tolist() == want, divs
+    h = A.PairHistogram(n, counts=torch.from_numpy(m).cuda())
+    with pytest.raises(ZeroDivisionError):
+        h.turn_into_probabilities_by_dividing_all_elements_by_given_number(0)

@@ -69,6 +69,29 @@ def test_pair_histogram_from_counts():
     assert h.upper().tolist() == [1, 2, 3, 6, 7, 11]
 
 
+def test_pair_histogram_divisors():
+    """ADVICE r05: a zero divisor raises ZeroDivisionError as the reference's `/` does (analysis.py:86-88);
+    negative and fractional divisors divide like the reference, pending or applied, host counts or not."""
+    A = pkg("analysis")
+    m = np.arange(16, dtype=np.int64).reshape(4, 4)
+    ref = {(i, j): int(m[i, j]) for i in range(4) for j in range(i + 1, 4)}
+    for div in (0, 0.0):
+        h = A.PairHistogram(4, counts=m)
+        with pytest.raises(ZeroDivisionError):
+            h.turn_into_probabilities_by_dividing_all_elements_by_given_number(div)
+        with pytest.raises(ZeroDivisionError):
+            A.PairHistogram(4).turn_into_probabilities_by_dividing_all_elements_by_given_number(div)
+    A.PairHistogram(1).turn_into_probabilities_by_dividing_all_elements_by_given_number(0)   # no pairs: no division
+    for divs in ([-4], [2.5], [-3, 7], [10 ** 30]):
+        h = A.PairHistogram(4, counts=m)
+        for d in divs:
+            h.turn_into_probabilities_by_dividing_all_elements_by_given_number(d)
+        want = dict(ref)
+        for d in divs:
+            want = {kk: v / d for kk, v in want.items()}
+        assert h.get_dict() == want
+
+
 def test_shard_range_covers_exactly():
     D = pkg("distributed")
     for S in (0, 1, 7, 10000, 10 ** 6 + 3):
