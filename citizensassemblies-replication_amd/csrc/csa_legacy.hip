@@ -2847,9 +2847,13 @@ struct Pair2Plan {
     int grid = 0, lmax = 0;  // persistent workgroups; leftover tiles (pooled over the XCDs)
 };
 
-// alone (CSA_PAIR_ALONE): no draw runs beside this launch, so the kernel fastest alone is taken --
-// this one wherever it applies (n = 1727: 0.59 vs 0.68 ms per 10^6 panels, 0.50 vs 0.44 of the fp4
-// peak; profiles/r05_pair_alone.txt)
+// alone (CSA_PAIR_ALONE): no draw runs beside this launch, so the kernel fastest alone is taken.  This
+// one wins alone only with several tiles per side and enough panel blocks to amortise its persistent
+// grid (n = 1727: 0.60 vs 0.68 ms per 10^6 panels, 0.19 vs 0.20 per 2^18, level at 2^17, 0.053 vs
+// 0.043 ms per 10^4; n <= 200 level at 10^6 and 4.5x slower at 10^4; profiles/r06_pair_alone/): below
+// kP2AloneMinBlocks or kP2AloneMinTiles tiles per side the split kernel stays.  CSA_PAIR_ALONE_MIN_BLOCKS overrides the block bound (A/B).
+constexpr uint64_t kP2AloneMinBlocks = 2048;  // 131072 panels: level there, the tile kernel ahead from 262144
+constexpr int kP2AloneMinTiles = 4;           // n > 768
 bool pair2_plan(int32_t n, uint64_t n_blocks, uint32_t engine, bool shared, Pair2Plan &q, bool alone = false) {
     if (engine != CSA_PAIR_FP4 || n_blocks == 0 || n_blocks > kP2MaxBlocks) return false;
     const char *e = getenv("CSA_PAIR_KERNEL");
@@ -2871,6 +2875,11 @@ bool pair2_plan(int32_t n, uint64_t n_blocks, uint32_t engine, bool shared, Pair
     q.M.nblk = n_blocks;
     q.grid = cus;
     q.lmax = q.M.leftovers();  // pooled leftover tiles (each in pieces(lmax) int32 partial slots)
+    static const uint64_t alone_min_blocks = [] {
+        const char *v = getenv("CSA_PAIR_ALONE_MIN_BLOCKS");
+        return v ? (uint64_t)strtoull(v, nullptr, 10) : kP2AloneMinBlocks;
+    }();
+    alone = alone && n_blocks >= alone_min_blocks && q.M.nbt >= kP2AloneMinTiles;
     return force == 2 || alone || q.M.ntri >= cus;
 }
 
