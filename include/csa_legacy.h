@@ -294,7 +294,9 @@ int csa_transpose_count_async(const uint64_t *d_panels, uint64_t n_panels, int32
  * same 512-register per-CU form either way (measured faster beside the draws than
  * the 256-register form, which CSA_P2_NB=2 still selects).  engine | CSA_PAIR_ALONE
  * is the opposite hint: nothing runs beside the launch (a serial caller's last
- * batch), so the kernel fastest alone is taken (the per-CU kernel at any n). */
+ * batch), so the kernel fastest alone is taken: the per-CU kernel from 2048 panel
+ * blocks and 4 tiles per side (n > 768), the split kernel below (measured,
+ * profiles/r06_pair_alone/). */
 #define CSA_PAIR_FP4 0u
 #define CSA_PAIR_I8 1u
 #define CSA_PAIR_OVERWRITE 0x100u
