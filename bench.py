@@ -330,6 +330,11 @@ def run_job(args, world, rank, dev, torch, dist, A, Dd, enc, k, S, inst_dir, pip
     xchg = Dd.PanelExchange(n_max, W, world, dev, redraw=(enc.handle, k, args.seed, 0)
                             if args.exchange == "keys" else None) if world > 1 else None
 
+    # XT from the draw's fused pack (as the weak-scaling step): a ring of XT buffers, the draw of chunk j
+    # waiting for the pairs of chunk j - ring (long done), the counts the pair diagonal at the end
+    xt_draw = want_pairs and args.xt_from == "draw" and args.draw_streams == 1 and pipe.xt_fused()
+    xring = [pipe.xt] + [torch.empty_like(pipe.xt) for _ in range(2)] if xt_draw else None
+
     def job(begin, count):
         steps = (count + S - 1) // S
         with torch.cuda.stream(stream):
@@ -337,8 +342,36 @@ def run_job(args, world, rank, dev, torch, dist, A, Dd, enc, k, S, inst_dir, pip
             pipe.counts.zero_()
             if want_pairs and count == 0:
                 pipe.pairs.zero_()
+        if xt_draw and steps:
+            drawn, counted = [], []
+
+            def count_chunk(j):
+                o, ln = j * S, min(S, count - j * S)
+                stream.wait_event(drawn[j])
+                pipe.xt = xring[j % len(xring)]
+                pipe.pair_counts(ln, overwrite=j == 0, shared=j + 1 < steps)
+                ev = torch.cuda.Event()
+                ev.record(stream)
+                counted.append(ev)
+
+            ds = draw_streams[0]
+            for j in range(steps):
+                o, ln = j * S, min(S, count - j * S)
+                if j >= len(xring):
+                    ds.wait_event(counted[j - len(xring)])
+                pipe.panels, pipe.hashes = panels_all[o * W:(o + ln) * W], hashes_all[2 * o:2 * (o + ln)]
+                pipe.xt = xring[j % len(xring)]
+                assert pipe.draw_xt(args.seed, begin + o, ln, stream=ds)
+                ev = torch.cuda.Event()
+                ev.record(ds)
+                drawn.append(ev)
+                if j:
+                    count_chunk(j - 1)
+            count_chunk(steps - 1)
+            pipe.counts_from_pairs()
+            pipe.xt = xring[0]
         drawn = []
-        for j in range(steps):
+        for j in range(0 if xt_draw else steps):
             o, ln = j * S, min(S, count - j * S)
             pipe.panels, pipe.hashes = panels_all[o * W:(o + ln) * W], hashes_all[2 * o:2 * (o + ln)]
             ds = draw_streams[j % len(draw_streams)]
@@ -346,7 +379,7 @@ def run_job(args, world, rank, dev, torch, dist, A, Dd, enc, k, S, inst_dir, pip
             ev = torch.cuda.Event()
             ev.record(ds)
             drawn.append(ev)
-        for j in range(steps):
+        for j in range(0 if xt_draw else steps):
             o, ln = j * S, min(S, count - j * S)
             stream.wait_event(drawn[j])
             pipe.panels, pipe.hashes = panels_all[o * W:(o + ln) * W], hashes_all[2 * o:2 * (o + ln)]
@@ -418,7 +451,9 @@ def run_job(args, world, rank, dev, torch, dist, A, Dd, enc, k, S, inst_dir, pip
                                    args.config, Pj, world, n_max, S, k, enc.n, "pairs+" if want_pairs else ""),
                    "job_panels": Pj, "chunk_panels": S, "instance": inst_dir,
                    "parallelism": "panel shards x%d" % world, "draw_kernel": draw_name,
-                   "pipeline": "every chunk's draw enqueued at once on the draw stream; counting follows per chunk"},
+                   "pipeline": ("chunk draws on the draw stream, each writing its XT operand (3-buffer ring); the "
+                                "pair kernel follows per chunk, the counts are the pair diagonal") if xt_draw else
+                               "every chunk's draw enqueued at once on the draw stream; counting follows per chunk"},
         "checks": checks,
         "draw_stats": draw_stats,
         "cpu_baseline": None,

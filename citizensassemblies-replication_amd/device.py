@@ -212,7 +212,9 @@ class DevicePipeline:
         with ``overwrite_pairs``; later chunks add theirs.  Ordered after everything already on the
         pipeline stream; on return the pipeline stream is ordered after every draw.  ``reset_counts``:
         the per-person counts are zeroed on the pipeline stream after the draws are enqueued (before
-        the first chunk's counting), so the draws do not wait for it."""
+        the first chunk's counting), so the draws do not wait for it.  With ``overwrite_pairs`` and
+        ``reset_counts`` on an instance whose draw writes XT itself (xt_fused), the chunks take
+        _draw_xt_chunks instead: no transpose pass, the counts from the pair diagonal."""
         import os
         import torch
         S, C, W = int(S), max(1, min(int(chunk), self.max_panels)), self.enc.W
@@ -228,6 +230,9 @@ class DevicePipeline:
         if st is None:
             st = self.draw_stream = torch.cuda.Stream(self.device)
         st.wait_stream(self.stream)
+        if chunks and self.want_pairs and overwrite_pairs and reset_counts and self.xt_fused() and \
+                os.environ.get("CSA_DRAW_XT", "1") != "0":
+            return self._draw_xt_chunks(seed, panel_begin, panels, hashes, chunks, st)
         own_p, own_h = self.panels, self.hashes
         try:
             drawn = []
@@ -250,6 +255,57 @@ class DevicePipeline:
                                      alone=j + 1 == len(chunks))
         finally:
             self.panels, self.hashes = own_p, own_h
+
+    def xt_fused(self):
+        """True when this instance's batch draw is a register kernel with a fused pack (draw_lane_kernel /
+        draw_solo_kernel), i.e. draw_xt can write the XT operand itself."""
+        f = getattr(self, "_xt_fused", None)
+        if f is None:
+            f = self._xt_fused = self.want_pairs and self.draw_kernel_name().startswith(("draw_lane", "draw_solo"))
+        return f
+
+    XT_RING = 3   # XT buffers of draw_count_chunks' fused form (the draw of chunk c reuses chunk c - 3's)
+
+    def _draw_xt_chunks(self, seed, panel_begin, panels, hashes, chunks, st):
+        """draw_count_chunks for instances whose draw writes XT (csa_draw_xt_async): chunk c's draw, on the
+        draw stream, writes its panels, hashes and XT (a ring of XT_RING buffers: the draw of chunk c waits
+        for the pairs of chunk c - XT_RING, which ran long before), and the pipeline stream runs only the
+        pair kernel of chunk c after its draw (stored for the first chunk, added after); the counts are the
+        pair matrix's diagonal at the end (stored) -- no transpose pass (csa_transpose_count_async)."""
+        import torch
+        W = self.enc.W
+        ring = getattr(self, "_xt_ring", None)
+        if ring is None or ring[0].numel() != self.xt.numel():
+            ring = self._xt_ring = [self.xt] + [torch.empty_like(self.xt) for _ in range(self.XT_RING - 1)]
+        own_p, own_h, own_xt = self.panels, self.hashes, self.xt
+        drawn, counted, fused = [], [], []
+        try:
+            def count(j):
+                off, ln = chunks[j]
+                self.stream.wait_event(drawn[j])
+                self.panels, self.xt = panels[off * W:(off + ln) * W], ring[j % len(ring)]
+                if not fused[j]:                       # (not expected: xt_fused() said the draw writes XT)
+                    self.transpose_count(ln)
+                self.pair_counts(ln, overwrite=j == 0, shared=j + 1 < len(chunks), alone=j + 1 == len(chunks))
+                ev = torch.cuda.Event()
+                ev.record(self.stream)
+                counted.append(ev)
+
+            for j, (off, ln) in enumerate(chunks):
+                if j >= len(ring):
+                    st.wait_event(counted[j - len(ring)])   # that chunk's pairs have read this XT buffer
+                self.panels, self.hashes = panels[off * W:(off + ln) * W], hashes[2 * off:2 * (off + ln)]
+                self.xt = ring[j % len(ring)]
+                fused.append(self.draw_xt(seed, panel_begin + off, ln, stream=st))
+                ev = torch.cuda.Event()
+                ev.record(st)
+                drawn.append(ev)
+                if j:
+                    count(j - 1)
+            count(len(chunks) - 1)
+            self.counts_from_pairs()
+        finally:
+            self.panels, self.hashes, self.xt = own_p, own_h, own_xt
 
     def run(self, seed, panel_begin, S, max_attempts=0, overwrite_pairs=False):
         """Enqueue the whole pass; results accumulate into counts / pairs / unique (pairs are

@@ -539,7 +539,8 @@ def _sharded_call(A, N, dist, enc, k, S, random_seed, world, begin, local, n_max
         pipe.counts, pipe.pairs = acc[:n], pairs
         try:
             if local:
-                pipe.draw_count_chunks(random_seed, begin, local, panels, hashes, C, overwrite_pairs=True)
+                pipe.draw_count_chunks(random_seed, begin, local, panels, hashes, C, overwrite_pairs=True,
+                                       reset_counts=True)
             else:
                 pairs.zero_()
         finally:

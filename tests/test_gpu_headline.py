@@ -151,3 +151,74 @@ def test_device_histogram_divisors(gpu_available):
     h = A.PairHistogram(n, counts=torch.from_numpy(m).cuda())
     with pytest.raises(ZeroDivisionError):
         h.turn_into_probabilities_by_dividing_all_elements_by_given_number(0)
+
+
+@pytest.mark.parametrize("name,k,S,chunk", [("sf_e_tight_110", 110, 9001, 1100), ("example_large_200", 200, 5003, 640),
+                                            ("sf_e_110", 110, 4000, 4000)])
+def test_chunked_xt_ring_vs_oracle(gpu_available, monkeypatch, name, k, S, chunk):
+    """draw_count_chunks' fused form (every chunk's draw writes its XT into a 3-buffer ring, the pair kernel
+    per chunk, counts from the diagonal at the end; more chunks than ring buffers, a ragged last chunk):
+    counts, pair counts and the distinct count against the C oracle, and equal to the transpose form
+    (CSA_DRAW_XT=0).  A single chunk goes through the same ring path (sf_e_110, chunk = S)."""
+    import torch
+    A = pkg("analysis")
+    Dv = pkg("device")
+    inst = pkg().read_instance(*inst_paths(name), k)
+    used = []
+    real = Dv.DevicePipeline._draw_xt_chunks
+
+    def spy(self, *a, **kw):
+        used.append(len(a[4]))
+        return real(self, *a, **kw)
+
+    monkeypatch.setattr(Dv.DevicePipeline, "_draw_xt_chunks", spy)
+    enc = pkg().encode(inst.categories, inst.agents)
+    # the multi-chunk entry (legacy_sample_device takes its one-chunk path only for S <= chunk; force the
+    # chunk loop through the pipeline directly)
+    pipe = Dv.DevicePipeline(enc, k, chunk, want_pairs=True, want_unique=True, pairs_buffer=True)
+    W = enc.W
+    panels = torch.empty(S * W, dtype=torch.int64, device="cuda")
+    hashes = torch.empty(2 * S, dtype=torch.int64, device="cuda")
+    pipe.reset(pairs=False)
+    pipe.draw_count_chunks(13, 0, S, panels, hashes, chunk, overwrite_pairs=True, reset_counts=True)
+    torch.cuda.synchronize()
+    pipe.check_status()
+    assert used == [(S + chunk - 1) // chunk]
+    counts = pipe.counts.cpu().numpy()
+    pairs = pipe.pairs.view(enc.n, enc.n).cpu().numpy()
+    o = oracle_read(*inst_paths(name), k)
+    rc, opanels, _, _ = coracle.draw(o, k, 13, 0, S)
+    assert rc == 0
+    assert np.array_equal(panels.cpu().numpy().view(np.uint64).reshape(S, W), opanels)
+    assert np.array_equal(counts, coracle.counts(opanels, o.n))
+    assert np.array_equal(np.triu(pairs), np.triu(coracle.pairs(opanels, o.n)))
+    monkeypatch.setenv("CSA_DRAW_XT", "0")
+    pipe2 = Dv.DevicePipeline(enc, k, chunk, want_pairs=True, want_unique=True, pairs_buffer=True)
+    pipe2.reset(pairs=False)
+    pipe2.draw_count_chunks(13, 0, S, panels, hashes, chunk, overwrite_pairs=True, reset_counts=True)
+    torch.cuda.synchronize()
+    assert used == [(S + chunk - 1) // chunk]                  # the transpose form this time
+    assert np.array_equal(pipe2.counts.cpu().numpy(), counts)
+    assert np.array_equal(np.triu(pipe2.pairs.view(enc.n, enc.n).cpu().numpy()), np.triu(pairs))
+
+
+@pytest.mark.parametrize("config,job,chunk", [("sf_e_110", 70001, 16000), ("example_large_200", 50001, 9000)])
+def test_bench_job_xt_from_draw_equals_transpose(gpu_available, config, job, chunk):
+    """bench.py --job-panels with the draw writing XT (default, 3-buffer ring, counts from the diagonal) and
+    with xt_count_kernel (--xt-from count): the same count and pair-triangle digests, distinct count and
+    draw statistics."""
+    import json
+    import subprocess
+    import sys
+    from conftest import REPO
+    out = {}
+    for mode in ("draw", "count"):
+        r = subprocess.run([sys.executable, "bench.py", "--config", config, "--job-panels", str(job), "--panels",
+                            str(chunk), "--warmup", "1", "--no-cpu-baseline", "--no-api", "--xt-from", mode],
+                           cwd=REPO, capture_output=True, text=True, timeout=240)
+        assert r.returncode == 0, r.stderr[-2000:]
+        out[mode] = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert "XT" in out["draw"]["config"]["pipeline"] and "XT" not in out["count"]["config"]["pipeline"]
+    for key in ("job_unique", "job_count_sum", "job_pair_sum", "job_counts_sha256", "job_pairs_triu_sha256"):
+        assert out["draw"]["checks"][key] == out["count"]["checks"][key], key
+    assert out["draw"]["draw_stats"] == out["count"]["draw_stats"]
