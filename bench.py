@@ -790,7 +790,8 @@ def main():
                             "rate the kernel's class mix allows (tools/valu_budget.py: single-issue VALU 4.3, "
                             "dual-issue 2.47 SIMD cycles per wave-instruction, tools/coissue.hip); issue_frac_2cyc "
                             "is the same count priced at 2 cycles per wave-instruction") % ("2k B of pick list per panel" if split else
-                                             "8W + 16 B of packed panel and hash per panel")
+                                             "8W + 16 B of packed panel and hash%s per panel" % (
+                                                 " + n_pad / 8 B of the XT operand it writes" if any(fused_xt) else ""))
             if pmc_ok and pmc.get("draw_issue") and pmc.get("draw_kernel") == draw_name:
                 kernels["draw"]["pmc_issue"] = pmc["draw_issue"]
                 roof["issue_frac_2cyc"] = pmc["draw_issue"].get("valu_issue_frac")
