@@ -46,6 +46,7 @@ SIGNATURES = {
     "csa_version": (ctypes.c_int, []),
     "csa_last_error": (ctypes.c_char_p, []),
     "csa_device_count": (ctypes.c_int, [_P]),
+    "csa_current_device": (ctypes.c_int, [_P]),
     "csa_instance_create": (ctypes.c_int, [_I32, _I32, _I32, _P, _P, _P, _P, _P]),
     "csa_instance_destroy": (None, [_P]),
     "csa_instance_info": (ctypes.c_int, [_P, _P, _P, _P, _P]),

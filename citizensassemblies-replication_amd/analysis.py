@@ -456,7 +456,7 @@ def legacy_sample_device(enc, k, S, random_seed, keep_panels=True, chunk=1 << 20
         # the distinct-count table (zero-filled on allocation, on this stream) before the draws: the
         # draw stream waits on this stream, and the distinct count's side stream on the draw stream
         table = getattr(enc, "_table", None)
-        if table is None:
+        if table is None or table.device != dev:
             table = enc._table = HashTable(S, dev)
         table.ensure(S)
         try:

@@ -2346,6 +2346,15 @@ int csa_device_count(int32_t *out) {
     return CSA_OK;
 }
 
+int csa_current_device(int32_t *out) {
+    if (!out) return fail(CSA_E_INVALID, "null out");
+    int d = -1;
+    hipError_t e = hipGetDevice(&d);
+    *out = d;
+    if (e != hipSuccess) return fail(CSA_E_HIP, "hipGetDevice: %s", hipGetErrorString(e));
+    return CSA_OK;
+}
+
 int csa_instance_create(int32_t n, int32_t C, int32_t F, const int32_t *person_feat, const int32_t *fmin,
                         const int32_t *fmax, const int32_t *feat_cat, csa_instance **out) {
     if (!out) return fail(CSA_E_INVALID, "null out");

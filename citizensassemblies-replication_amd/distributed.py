@@ -532,7 +532,7 @@ def _sharded_call(A, N, dist, enc, k, S, random_seed, world, begin, local, n_max
         A.reset_draw_stats(enc, st)
         if ex is None:  # one rank: its distinct-count table before the draws (see below)
             table = getattr(enc, "_table", None)
-            if table is None:
+            if table is None or table.device != dev:
                 table = enc._table = HashTable(local, dev)
             table.ensure(local)
         own_counts, own_pairs = pipe.counts, pipe.pairs

@@ -84,23 +84,30 @@ class EncodedInstance:
         self.pool = np.bincount(pf.ravel(), minlength=self.F).astype(np.int32) if self.n else \
             np.zeros(self.F, np.int32)
         self.rem0 = np.where(self.rem0 < 0, self.pool, self.rem0).astype(np.int32)
-        self._handle = None
+        self._handles = {}                   # HIP device index -> native instance on that device
 
     # -- native handle ---------------------------------------------------------------------
     @property
     def handle(self):
-        if self._handle is None:
-            import ctypes
-            L = N.lib()
+        """The native instance on the calling thread's current HIP device (created there on first use).
+        The stream-ordered entry points launch on the caller's stream, so an instance must live on the
+        device the call runs on: a sharded call runs on its rank's GPU without changing the caller's
+        current device, and a later call on another device gets an instance of its own."""
+        import ctypes
+        L = N.lib()
+        d = ctypes.c_int32(-1)
+        N.check(L.csa_current_device(ctypes.byref(d)))
+        h = self._handles.get(d.value)
+        if h is None:
             h = ctypes.c_void_p()
             N.check(L.csa_instance_create(self.n, self.C, self.F, N.ptr(self.person_feat), N.ptr(self.fmin),
                                           N.ptr(self.fmax), N.ptr(self.fcat), ctypes.byref(h)))
-            self._handle = h
+            self._handles[d.value] = h
             # the dicts' own "selected" / "remaining" counters are the draw's start state, as in
             # the reference's deep copies (analysis.py:147-148); the device default is 0 / pool
             if np.any(self.sel0 != 0) or not np.array_equal(self.rem0, self.pool):
                 N.check(L.csa_instance_set_state(h, N.ptr(self.sel0), N.ptr(self.rem0), None))
-        return self._handle
+        return h
 
     def release_device_buffers(self):
         """Drop the cached device pipeline / hash table (they are rebuilt on the next call)."""
@@ -108,9 +115,9 @@ class EncodedInstance:
         self.__dict__.pop("_table", None)
 
     def close(self):
-        if self._handle is not None:
-            N.lib().csa_instance_destroy(self._handle)
-            self._handle = None
+        handles, self._handles = getattr(self, "_handles", {}), {}
+        for h in handles.values():
+            N.lib().csa_instance_destroy(h)
 
     def __del__(self):
         try:

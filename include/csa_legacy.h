@@ -55,6 +55,10 @@ typedef struct csa_instance csa_instance;
 int csa_version(void);                 /* ABI version, currently 1 */
 const char *csa_last_error(void);      /* thread-local message of the last failing call */
 int csa_device_count(int32_t *out);    /* HIP devices visible to this process */
+/* The calling thread's current HIP device (hipGetDevice).  An instance lives on the device that was
+ * current at csa_instance_create; the stream-ordered entry points run on the caller's stream, so a
+ * caller keeps one instance per device it launches on (the Python layer does: EncodedInstance.handle). */
+int csa_current_device(int32_t *out);
 
 /* Encode an instance (replaces read_instance's dicts, analysis.py:108-138).
  * person_feat: n*C global feature ids (row p = agent p, column c = category c);

@@ -370,3 +370,46 @@ def test_chunk_plan_rounds():
         assert sum(sizes) == S and all(0 < c <= C for c in sizes)
         if S > R:
             assert sizes[-2] == R and all(c % R == 0 for c in sizes[:-1])
+
+
+def test_encoding_handle_per_device(monkeypatch):
+    """EncodedInstance.handle is the native instance on the CURRENT HIP device, created there on first use
+    (csa_current_device): a sharded call that runs on its rank's GPU without changing the caller's device,
+    and a later call on another device, never launch on an instance of another device.  A fake library
+    stands in for the C ABI (no GPU here)."""
+    import ctypes
+    P = pkg()
+    N = pkg("_native")
+    state = {"dev": 0, "made": [], "destroyed": [], "set_state": []}
+
+    class Fake:
+        def csa_current_device(self, out):
+            ctypes.cast(out, ctypes.POINTER(ctypes.c_int32))[0] = state["dev"]
+            return 0
+
+        def csa_instance_create(self, n, C, F, pf, fmin, fmax, fcat, out):
+            h = 1000 + len(state["made"])
+            state["made"].append((state["dev"], h))
+            ctypes.cast(out, ctypes.POINTER(ctypes.c_void_p))[0] = h
+            return 0
+
+        def csa_instance_set_state(self, h, sel, rem, present):
+            state["set_state"].append(h.value)
+            return 0
+
+        def csa_instance_destroy(self, h):
+            state["destroyed"].append(h.value)
+
+    monkeypatch.setattr(N, "lib", lambda: Fake())
+    cats = {"c": {"a": {"min": 0, "max": 2, "selected": 1}, "b": {"min": 0, "max": 2}}}
+    enc = P.encode(cats, {0: {"c": "a"}, 1: {"c": "b"}})
+    h0 = enc.handle
+    assert enc.handle.value == h0.value and len(state["made"]) == 1      # cached on device 0
+    state["dev"] = 3
+    h3 = enc.handle
+    assert h3.value != h0.value and state["made"][-1] == (3, h3.value)   # a new instance on device 3
+    state["dev"] = 0
+    assert enc.handle.value == h0.value and len(state["made"]) == 2
+    assert state["set_state"] == [h0.value, h3.value]                    # the dicts' start state on each
+    enc.close()
+    assert sorted(state["destroyed"]) == sorted([h0.value, h3.value])
